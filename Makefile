@@ -1,0 +1,33 @@
+# Builds the gfx950 engine (lambdafs_amd/libhrs.so) and the test-only CPU
+# oracle (oracle/liboracle.so). `python -c "import __graft_entry__ as g; g.build()"`
+# runs the same recipe.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+CC       ?= gcc
+
+LIB      := lambdafs_amd/libhrs.so
+ORACLE   := oracle/liboracle.so
+SRCS     := lambdafs_amd/csrc/hrs_api.cpp lambdafs_amd/csrc/hrs_kernels.hip
+HDRS     := include/hrs.h lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp
+
+all: $(LIB) $(ORACLE)
+
+build/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+build/hrs_kernels.o: lambdafs_amd/csrc/hrs_kernels.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): build/hrs_api.o build/hrs_kernels.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+
+$(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
+	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/rs_oracle.c
+
+clean:
+	rm -rf build $(LIB) $(ORACLE)
+
+.PHONY: all clean

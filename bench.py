@@ -1,0 +1,255 @@
+"""Benchmark of the MI355X RS engine on BASELINE.json's metric.
+
+Metric: "RS encode+decode GiB/s device-resident; 1/2/4/8 MI355X; %HBM roofline".
+Workload (configs[2]): RS(10,4) encode + 1-erasure decode, 1 MiB cells.
+One step = one pass of the hot path over one batch resident in HBM:
+  encode  : parity of all S stripes           (ReedSolomonCode.encodeBulk)
+  decode  : data shard 0 (hops location 4) of all S stripes from the k
+            survivors locationsToReadForDecode picks (ReedSolomonCode.decodeBulk)
+S = 1024 stripes per GPU (weak scaling: each rank owns its own stripe range;
+no data crosses xGMI). RCCL carries only the coding matrices (broadcast from
+rank 0) and the barriers around the timed region.
+
+value = user-data bytes (k * L per stripe, counted once for the encode and
+once for the decode) of all ranks / max-over-ranks wall time, in GiB/s.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from lambdafs_amd import HipReedSolomonCode, device  # noqa: E402
+
+GiB = float(1 << 30)
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU")
+    ap.add_argument("--cell", type=int, default=1 << 20, help="cell bytes (bufSize)")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--p", type=int, default=4)
+    ap.add_argument("--cpu-stripes", type=int, default=48, help="stripes in the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify a sample against the oracle after timing")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def broadcast_matrix(m, world, local):
+    """Rank 0's coding matrix over RCCL; every rank checks it against its own."""
+    t = torch.from_numpy(np.ascontiguousarray(m)).to(f"cuda:{local}")
+    if world > 1:
+        dist.broadcast(t, src=0)
+    got = t.cpu().numpy()
+    if not np.array_equal(got, m):
+        raise RuntimeError("broadcast coding matrix differs from the local one")
+    return got
+
+
+def cpu_baseline(k, p, L, nstripes):
+    """Restated reference CPU path (oracle/: C transcription of
+    ReedSolomonCode.encodeBulk + per-byte decodeBulk 5-arg) on a bounded
+    sample of the same workload, stripes spread over host threads."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import rs_oracle as C
+    C.lib()
+    n = k + p
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    rng = np.random.default_rng(0x5EED0003)
+    data = [[rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] for _ in range(min(nstripes, cores))]
+    erased = [p]
+    to_read = sorted(C.locations_to_read(k, p, erased))
+    ntr = [x for x in range(n) if x not in to_read]
+
+    def one(i):
+        src = [x.copy() for x in data[i % len(data)]]  # encodeBulk zeroes its inputs, like the Java
+        par = [np.zeros(L, np.uint8) for _ in range(p)]
+        C.encode_bulk_ptrs(k, p, C.rowptrs(src), C.rowptrs(par), L)
+        stripe = par + data[i % len(data)]
+        reads = [stripe[j] if j in to_read else np.zeros(L, np.uint8) for j in range(n)]
+        out = [np.zeros(L, np.uint8)]
+        C.decode_bulk5_ptrs(k, p, C.rowptrs(reads), C.rowptrs(out), erased, to_read, ntr, L)
+        return bool((out[0] == data[i % len(data)][0]).all())
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        ok = all(ex.map(one, range(nstripes)))
+    dt = time.perf_counter() - t0
+    if not ok:
+        raise RuntimeError("CPU baseline round trip failed")
+    return {
+        "value": round(2 * k * L * nstripes / GiB / dt, 4),
+        "unit": "GiB/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{nstripes} stripes RS({k},{p}) x {L >> 10} KiB cells, encode + 1-erasure decode, "
+                  f"{cores} threads, {dt:.1f} s wall",
+    }
+
+
+def load_traffic(kernel):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    k, p, L, S = args.k, args.p, args.cell, args.stripes
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=local)
+
+    # coding matrices: built on rank 0, broadcast over RCCL, checked everywhere
+    erased = [p]  # data shard 0 = hops location p
+    to_read = sorted(code.locationsToReadForDecode(erased))
+    ntr = [x for x in range(n) if x not in to_read]
+    G = broadcast_matrix(code.encodeMatrix(), world, local)
+    D = broadcast_matrix(code.decodeMatrix(erased, ntr), world, local)
+    D_live = np.ascontiguousarray(D[:, to_read])
+
+    # synthetic stripes, resident in HBM before timing: [S, n, L] hops order
+    gen = torch.Generator(device=f"cuda:{local}")
+    gen.manual_seed(0x5EED0003 + rank)
+    stripes = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device=f"cuda:{local}", generator=gen)
+    out = torch.empty((S, len(erased), L), dtype=torch.uint8, device=f"cuda:{local}")
+    in_rows = [stripes[:, loc, :] for loc in to_read]
+    out_rows = [out[:, 0, :]]
+    assert G.shape == (p, k)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        device.encode_stripes(code, stripes)
+        if ev is not None:
+            ev[1].record()
+        device.apply_rows(code, D_live, in_rows, out_rows)
+        if ev is not None:
+            ev[2].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+
+    # correctness of what was timed: the decode must reproduce data shard 0
+    ok = bool(torch.equal(out[:, 0], stripes[:, p]))
+    if args.check:
+        from oracle import rs_oracle as C
+        host = stripes[S // 2].cpu().numpy()
+        ref = np.stack(C.encode_bulk(k, p, [host[p + c] for c in range(k)]))
+        ok &= bool((host[:p] == ref).all())
+    okt = torch.tensor([1 if ok else 0], device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if not bool(okt.item()):
+        raise RuntimeError("benchmark output failed its round-trip check")
+
+    user_bytes = 2 * k * L * S * world * args.steps
+    enc_bytes = (k + p) * L * S  # algorithmic bytes per encode launch (read k, write p)
+    dec_bytes = (k + len(erased)) * L * S
+    enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
+    dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
+    kernel = f"encode_static_kernel<{k},{p}>"
+    res = None
+    if rank == 0:
+        res = {
+            "metric": "RS encode+decode GiB/s device-resident; 1/2/4/8 MI355X; %HBM roofline",
+            "value": round(user_bytes / GiB / elapsed, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint uniform bytes, seeded per rank)",
+            "config": {
+                "workload": f"RS({k},{p}) encode + 1-erasure decode (data shard 0), {L >> 10} KiB cells, "
+                            f"{S} stripes/GPU, device-resident",
+                "stripes_per_gpu": S, "cell_bytes": L, "k": k, "p": p,
+                "parallelism": f"stripe-sharded x{world} (RCCL: matrix broadcast + barriers only)",
+            },
+            "encode_GiBps_per_gpu": round(k * L * S / GiB / (enc_ms * 1e-3), 3),
+            "decode_GiBps_per_gpu": round(k * L * S / GiB / (dec_ms * 1e-3), 3),
+            "roofline": {
+                "kernel": kernel,
+                "bound": "hbm",
+                "achieved": round(enc_gbps, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
+                "traffic": load_traffic(kernel),
+                "avg_launch_ms": round(enc_ms, 4),
+                "algorithmic_bytes_per_launch": enc_bytes,
+            },
+            "decode_roofline": {
+                "kernel": "bitsliced_kernel<1>", "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(dec_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(dec_ms, 4),
+                "algorithmic_bytes_per_launch": dec_bytes,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * hrs.h — C ABI of the MI355X-native Reed-Solomon engine (libhrs.so).
+ *
+ * This is the drop-in boundary behind the hops codec plugin surface
+ * `io.hops.erasure_coding.ErasureCode` (hadoop-hdfs-project/hadoop-hdfs/src/
+ * main/java/io/hops/erasure_coding/ErasureCode.java:25-182). A JNI shim
+ * (lambdafs_amd/jni/) maps the Java class
+ * `io.hops.erasure_coding.HipReedSolomonCode extends ErasureCode` onto these
+ * entry points exactly as the existing native precedent
+ * `NativeReedSolomonCode` maps onto libhadoop's ISA-L shim
+ * (hops-erasure-coding/.../NativeReedSolomonCode.java:55-152 ->
+ *  hadoop-common/src/main/native/src/org/apache/hadoop/io/erasurecode/
+ *  jni_rs_encoder.c:45-63, jni_rs_decoder.c:35-77).
+ *
+ * Semantics are those of the Java `rs` codec, `ReedSolomonCode`
+ * (hops-erasure-coding/src/main/java/io/hops/erasure_coding/
+ * ReedSolomonCode.java), bit-exact:
+ *   - GF(2^8), primitive polynomial 0x11D, alpha = 2;
+ *   - stripe locations in hops order: [0, p) parity, [p, p+k) data;
+ *   - encode  = ReedSolomonCode.encodeBulk   (ReedSolomonCode.java:103-125);
+ *   - decode  = ReedSolomonCode.decodeBulk 5-arg (ReedSolomonCode.java:191-211);
+ *   - decode3 = ReedSolomonCode.decodeBulk 3-arg (ReedSolomonCode.java:168-185).
+ *
+ * Conventions: no JNI or torch types; plain pointers and sizes. Every
+ * function returns HRS_OK (0) on success and a nonzero hrs_status otherwise;
+ * the JNI shim turns a nonzero status into java.io.IOException
+ * (HRS_ETOOMANY into io.hops.erasure_coding.TooManyErasedLocations), as
+ * jni_rs_encoder.c:51 THROWs. A handle is not thread-safe (like the Java
+ * ReedSolomonCode, whose scratch arrays are per instance,
+ * ReedSolomonCode.java:36-38); distinct handles are fully concurrent.
+ */
+#ifndef HRS_H_
+#define HRS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int hrs_status;
+enum {
+  HRS_OK = 0,
+  HRS_EINVAL = 1,    /* bad argument (IllegalArgumentException / assert in Java) */
+  HRS_ETOOMANY = 2,  /* ErasureCode.java:105-111 TooManyErasedLocations */
+  HRS_EDEVICE = 3,   /* HIP runtime failure (no GPU, launch or copy error) */
+  HRS_ENOMEM = 4,    /* device or pinned-host allocation failed */
+  HRS_EALIGN = 5     /* device-batch rows not 16-byte aligned (see hrs_*_dev) */
+};
+
+typedef struct hrs_codec hrs_codec;
+
+#define HRS_DEVICE_NONE (-2)
+
+typedef struct hrs_opts {
+  int device;         /* HIP device ordinal; -1 = current device; HRS_DEVICE_NONE =
+                         host-only handle (matrix/location queries; coding calls
+                         fail with HRS_EDEVICE) */
+  int reserved[7];    /* must be zero */
+} hrs_opts;
+
+/* ---- lifecycle (ReedSolomonCode() + init(Codec), ReedSolomonCode.java:45-82) ---- */
+
+/* Builds the generator polynomial and encode matrix for RS(stripe_size,
+ * parity_size). Requires stripe_size >= 1, parity_size >= 1 and
+ * stripe_size + parity_size < 256 (ReedSolomonCode.java:57). opts may be NULL. */
+hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out);
+void hrs_destroy(hrs_codec* codec);
+/* Last error message of this handle ("" if none); handle may be NULL for create errors. */
+const char* hrs_last_error(const hrs_codec* codec);
+const char* hrs_version(void);
+
+/* ErasureCode.stripeSize()/paritySize()/symbolSize() (ReedSolomonCode.java:213-226). */
+int hrs_stripe_size(const hrs_codec* codec);
+int hrs_parity_size(const hrs_codec* codec);
+int hrs_symbol_size(const hrs_codec* codec);
+
+/* ---- host helpers (no device work) ---- */
+
+/* ErasureCode.locationsToReadForDecode (ErasureCode.java:89-113): writes the
+ * k = stripe_size highest-index locations not in `erased` to to_read, in
+ * descending order, as the Java list is built. HRS_ETOOMANY if fewer than k
+ * survive. */
+hrs_status hrs_locations_to_read(const hrs_codec* codec, const int* erased, int num_erased,
+                                 int* to_read);
+
+/* p x k encode matrix G (row-major): parity_r = XOR_c G[r][c] * data_c. */
+hrs_status hrs_encode_matrix(const hrs_codec* codec, uint8_t* g);
+
+/* num_erased x n decode matrix D (row-major, n = k + p, hops order):
+ * out_i = XOR_l D[i][l] * in_l.
+ * zero_not_to_read = 1: decodeBulk 5-arg semantics (ReedSolomonCode.java:144-166,
+ *   191-211): locations in not_to_read are zeroed, m = num_not_to_read
+ *   syndromes, erased locations absent from not_to_read decode to 0.
+ * zero_not_to_read = 0: decodeBulk 3-arg semantics (ReedSolomonCode.java:168-185):
+ *   not_to_read is the erased list itself, nothing is zeroed.
+ * Locations must be distinct and in [0, n). */
+hrs_status hrs_decode_matrix(const hrs_codec* codec, const int* erased, int num_erased,
+                             const int* not_to_read, int num_not_to_read, int zero_not_to_read,
+                             uint8_t* d);
+
+/* ---- synchronous host-buffer calls: the JNI path (GetPrimitiveArrayCritical rows) ---- */
+
+/* ReedSolomonCode.encodeBulk(byte[][] inputs, byte[][] outputs):
+ * inputs[k] rows and outputs[p] rows, each `len` bytes, host memory.
+ * Outputs are fully overwritten. Unlike the Java method (whose bulk
+ * remainder zeroes `inputs`, GaloisField.java:326-338) inputs are left
+ * untouched; the Java/Python shims restore that side effect when asked. */
+hrs_status hrs_encode(hrs_codec* codec, const uint8_t* const* inputs, uint8_t* const* outputs,
+                      size_t len);
+
+/* ReedSolomonCode.decodeBulk(readBufs, writeBufs, erased, toRead, notToRead)
+ * (ReedSolomonCode.java:191-211): read_bufs[n] in hops order (a row may be
+ * NULL when its location is in not_to_read — the reference feeds zeros
+ * there, StripeReader.java:111-120); write_bufs[num_erased], row i = value at
+ * erased[i]. to_read is accepted for interface parity; like the Java code the
+ * result depends only on erased and not_to_read. */
+hrs_status hrs_decode(hrs_codec* codec, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                      const int* erased, int num_erased, const int* to_read, int num_to_read,
+                      const int* not_to_read, int num_not_to_read, size_t len);
+
+/* ReedSolomonCode.decodeBulk(readBufs, writeBufs, erasedLocation)
+ * (ReedSolomonCode.java:168-185): all n rows are read as given. */
+hrs_status hrs_decode3(hrs_codec* codec, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                       const int* erased, int num_erased, size_t len);
+
+/* ---- device-resident batches (the MI355X hot path) ----
+ * Row pointers are DEVICE pointers for stripe 0; stripe s of row r lives at
+ * rows[r] + s * stride. `stream` is a hipStream_t (NULL = the null stream).
+ * Calls are asynchronous on `stream`. For the vector path every row pointer
+ * and stride must be 16-byte aligned; otherwise a byte-granular kernel runs. */
+
+/* Encode nstripes stripes: in_rows[k] data rows -> out_rows[p] parity rows. */
+hrs_status hrs_encode_dev(hrs_codec* codec, const uint8_t* const* in_rows, size_t in_stride,
+                          uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
+                          void* stream);
+
+/* decodeBulk 5-arg over nstripes stripes: rows[n] in hops order (entries for
+ * not_to_read locations may be NULL), out_rows[num_erased]. */
+hrs_status hrs_decode_dev(hrs_codec* codec, const uint8_t* const* rows, size_t in_stride,
+                          uint8_t* const* out_rows, size_t out_stride, const int* erased,
+                          int num_erased, const int* not_to_read, int num_not_to_read, size_t len,
+                          size_t nstripes, void* stream);
+
+/* Generic GF(2^8) matrix x rows: out_o = XOR_i m[o * nin + i] * in_i (m on
+ * the host, row-major nout x nin). Used with coding matrices broadcast over
+ * RCCL, and by the 3-arg decode. nin, nout in [1, 255]. */
+hrs_status hrs_apply_dev(hrs_codec* codec, const uint8_t* m, int nout, int nin,
+                         const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
+                         size_t out_stride, size_t len, size_t nstripes, void* stream);
+
+/* Kernel selection for tests and benchmarks: 0 = auto (default), 1 = force
+ * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel. */
+hrs_status hrs_set_kernel_mode(hrs_codec* codec, int mode);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HRS_H_ */

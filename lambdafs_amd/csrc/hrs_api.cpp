@@ -1,0 +1,538 @@
+// C ABI of libhrs (include/hrs.h): codec lifecycle, coding matrices, the
+// decode-matrix cache, and dispatch of the gfx950 kernels.
+//
+// Mirrors the Java codec plugin surface io.hops.erasure_coding.ErasureCode
+// (hadoop-hdfs/.../io/hops/erasure_coding/ErasureCode.java:25-182) as
+// implemented by ReedSolomonCode (hops-erasure-coding/.../ReedSolomonCode.java).
+// Matrices are derived in closed form here; the CPU restatement of the
+// reference's per-byte loops lives only in oracle/ (test infrastructure).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hrs.h"
+#include "gf256.hpp"
+#include "hrs_internal.hpp"
+
+using hrs::RowArgs;
+namespace gf = hrs::gf;
+
+struct hrs_codec {
+  int k = 0;
+  int p = 0;
+  int n = 0;
+  int device = 0;
+  int kernel_mode = 0;
+  std::vector<uint8_t> g;  // p x k
+  hipStream_t stream = nullptr;
+  uint8_t* scratch = nullptr;  // device scratch for the host-buffer calls
+  size_t scratch_bytes = 0;
+  std::map<std::vector<int>, std::vector<uint8_t>> decode_cache;
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+hrs_status fail(hrs_codec* c, hrs_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c)
+    c->err = buf;
+  else
+    g_create_error = buf;
+  return st;
+}
+
+hrs_status hip_fail(hrs_codec* c, hipError_t e, const char* what) {
+  return fail(c, HRS_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+// Keeps the caller's current device across a call on codec->device.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (dev < 0) {  // host-only handle
+      ok = false;
+      return;
+    }
+    if (hipGetDevice(&prev) != hipSuccess) {
+      ok = false;
+      return;
+    }
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) ok = false;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// ---------------------------------------------------------- GF linear algebra
+
+// In-place Gauss-Jordan inverse of an m x m matrix over GF(2^8). False if singular.
+bool gf_invert(std::vector<uint8_t>& a, int m) {
+  std::vector<uint8_t> inv(static_cast<size_t>(m) * m, 0);
+  for (int i = 0; i < m; ++i) inv[i * m + i] = 1;
+  for (int col = 0; col < m; ++col) {
+    int piv = -1;
+    for (int r = col; r < m; ++r)
+      if (a[r * m + col]) {
+        piv = r;
+        break;
+      }
+    if (piv < 0) return false;
+    if (piv != col)
+      for (int j = 0; j < m; ++j) {
+        std::swap(a[piv * m + j], a[col * m + j]);
+        std::swap(inv[piv * m + j], inv[col * m + j]);
+      }
+    const uint8_t s = gf::inv(a[col * m + col]);
+    for (int j = 0; j < m; ++j) {
+      a[col * m + j] = gf::mul(a[col * m + j], s);
+      inv[col * m + j] = gf::mul(inv[col * m + j], s);
+    }
+    for (int r = 0; r < m; ++r) {
+      if (r == col || a[r * m + col] == 0) continue;
+      const uint8_t f = a[r * m + col];
+      for (int j = 0; j < m; ++j) {
+        a[r * m + j] ^= gf::mul(f, a[col * m + j]);
+        inv[r * m + j] ^= gf::mul(f, inv[col * m + j]);
+      }
+    }
+  }
+  a.swap(inv);
+  return true;
+}
+
+// Decode matrix in closed form (see hrs.h). With x_j = alpha^ntr[j] and
+// syndromes S_i = sum_l A[i][l] d_l, A[i][l] = alpha^(i*l) (0 where zeroed),
+// the reference solves V z = S with V[i][j] = x_j^i
+// (GaloisField.java:232-246; ReedSolomonCode.java:127-142), so z = V^-1 A d.
+hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
+                               int zero_ntr, std::vector<uint8_t>& d) {
+  const int n = c->n;
+  d.assign(static_cast<size_t>(ne) * n, 0);
+  if (ne == 0 || nn == 0) return HRS_OK;
+  std::vector<char> in_ntr(n, 0);
+  for (int j = 0; j < nn; ++j) {
+    if (ntr[j] < 0 || ntr[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range [0,%d)", ntr[j], n);
+    if (in_ntr[ntr[j]]) return fail(c, HRS_EINVAL, "duplicate location %d", ntr[j]);
+    in_ntr[ntr[j]] = 1;
+  }
+  for (int t = 0; t < ne; ++t)
+    if (erased[t] < 0 || erased[t] >= n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  const int m = nn;
+  std::vector<uint8_t> v(static_cast<size_t>(m) * m);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) v[i * m + j] = gf::alpha_pow(static_cast<long>(ntr[j]) * i);
+  if (!gf_invert(v, m)) return fail(c, HRS_EINVAL, "singular Vandermonde system");
+  for (int t = 0; t < ne; ++t) {
+    int j = -1;
+    for (int q = 0; q < nn; ++q)
+      if (ntr[q] == erased[t]) {
+        j = q;
+        break;
+      }
+    if (j < 0) continue;  // not in not_to_read: stays 0 (ReedSolomonCode.java:158-165)
+    for (int l = 0; l < n; ++l) {
+      if (zero_ntr && in_ntr[l]) continue;
+      uint8_t acc = 0;
+      for (int i = 0; i < m; ++i) acc ^= gf::mul(v[j * m + i], gf::alpha_pow(static_cast<long>(i) * l));
+      d[static_cast<size_t>(t) * n + l] = acc;
+    }
+  }
+  return HRS_OK;
+}
+
+const std::vector<uint8_t>* cached_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
+                                                 int zero_ntr, hrs_status* st) {
+  std::vector<int> key;
+  key.reserve(ne + nn + 3);
+  key.push_back(zero_ntr);
+  key.push_back(ne);
+  key.insert(key.end(), erased, erased + ne);
+  key.push_back(nn);
+  key.insert(key.end(), ntr, ntr + nn);
+  auto it = c->decode_cache.find(key);
+  if (it != c->decode_cache.end()) {
+    *st = HRS_OK;
+    return &it->second;
+  }
+  std::vector<uint8_t> d;
+  *st = build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, d);
+  if (*st != HRS_OK) return nullptr;
+  if (c->decode_cache.size() > 4096) c->decode_cache.clear();
+  return &(c->decode_cache[key] = std::move(d));
+}
+
+// ---------------------------------------------------------------- dispatch
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// out_o = XOR_i m[o][i] * in_i for every stripe. `static_kp` allows the
+// compile-time encode kernels when m is this codec's G and inputs are the k
+// data rows in order.
+hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                     size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len,
+                     size_t nstripes, hipStream_t s, bool static_kp) {
+  if (nout < 0 || nin < 0 || nout > 255 || nin > 255) return fail(c, HRS_EINVAL, "bad matrix shape %dx%d", nout, nin);
+  if (nout == 0 || len == 0 || nstripes == 0) return HRS_OK;
+  for (int o = 0; o < nout; ++o)
+    if (!out_rows[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  // Inputs whose coefficients are zero for every output contribute nothing:
+  // skip them (saves their HBM reads; exact, since 0 * x = 0).
+  std::vector<int> live;
+  for (int i = 0; i < nin; ++i) {
+    bool any = false;
+    for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
+    if (any) {
+      if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL but has nonzero coefficients", i);
+      live.push_back(i);
+    }
+  }
+  if (static_cast<int>(live.size()) != nin) static_kp = false;
+  bool vec_ok = (in_stride % 16 == 0) && (out_stride % 16 == 0);
+  for (int i : live) vec_ok &= aligned16(in_rows[i]);
+  for (int o = 0; o < nout; ++o) vec_ok &= aligned16(out_rows[o]);
+  const int mode = c->kernel_mode;
+  if (mode == 2) vec_ok = false;
+  if (mode != 0) static_kp = false;
+
+  const uint64_t nwin = vec_ok ? len / hrs::kWindowBytes : 0;
+  const uint64_t tail_off = nwin * hrs::kWindowBytes;
+  const uint64_t tail = len - tail_off;
+
+  if (live.empty()) {  // all-zero matrix: outputs are zero
+    for (int o = 0; o < nout; ++o)
+      for (size_t st = 0; st < nstripes; ++st) {
+        hipError_t e = hipMemsetAsync(out_rows[o] + st * out_stride, 0, len, s);
+        if (e != hipSuccess) return hip_fail(c, e, "hipMemsetAsync");
+      }
+    return HRS_OK;
+  }
+
+  if (static_kp && nwin > 0) {
+    RowArgs a{};
+    for (int i = 0; i < nin; ++i) a.in[i] = in_rows[i];
+    for (int o = 0; o < nout; ++o) a.out[o] = out_rows[o];
+    a.in_stride = in_stride;
+    a.out_stride = out_stride;
+    a.len = len;
+    a.nwin = nwin;
+    a.ntasks = nwin * nstripes;
+    a.nin = nin;
+    a.nout = nout;
+    bool handled = false;
+    hipError_t e = hrs::launch_static_encode(c->k, c->p, a, s, &handled);
+    if (e != hipSuccess) return hip_fail(c, e, "static encode launch");
+    if (handled) {
+      if (tail == 0) return HRS_OK;
+      std::vector<const uint8_t*> tin(nin);
+      std::vector<uint8_t*> tout(nout);
+      for (int i = 0; i < nin; ++i) tin[i] = in_rows[i] + tail_off;
+      for (int o = 0; o < nout; ++o) tout[o] = out_rows[o] + tail_off;
+      // tail < one window: run_apply sends it to the byte-granular kernel
+      return run_apply(c, m, nout, nin, tin.data(), in_stride, tout.data(), out_stride, tail, nstripes, s, false);
+    }
+  }
+
+  const int nlive = static_cast<int>(live.size());
+  for (int o0 = 0; o0 < nout; o0 += hrs::kMaxOut) {
+    const int no = std::min(hrs::kMaxOut, nout - o0);
+    for (int i0 = 0; i0 < nlive; i0 += hrs::kMaxIn) {
+      const int ni = std::min(hrs::kMaxIn, nlive - i0);
+      RowArgs a{};
+      for (int i = 0; i < ni; ++i) a.in[i] = in_rows[live[i0 + i]];
+      for (int o = 0; o < no; ++o) {
+        a.out[o] = out_rows[o0 + o];
+        for (int i = 0; i < ni; ++i) a.coef[o][i] = m[(o0 + o) * nin + live[i0 + i]];
+      }
+      a.in_stride = in_stride;
+      a.out_stride = out_stride;
+      a.nin = ni;
+      a.nout = no;
+      a.accumulate = i0 > 0;
+      if (nwin > 0) {
+        a.len = len;
+        a.nwin = nwin;
+        a.ntasks = nwin * nstripes;
+        hipError_t e = hrs::launch_bitsliced(a, s);
+        if (e != hipSuccess) return hip_fail(c, e, "bitsliced launch");
+      }
+      if (tail > 0) {
+        RowArgs b = a;
+        for (int i = 0; i < ni; ++i) b.in[i] = a.in[i] + tail_off;
+        for (int o = 0; o < no; ++o) b.out[o] = a.out[o] + tail_off;
+        b.len = tail;
+        b.nwin = 0;
+        b.ntasks = tail * nstripes;
+        hipError_t e = hrs::launch_bytewise(b, s);
+        if (e != hipSuccess) return hip_fail(c, e, "bytewise launch");
+      }
+    }
+  }
+  return HRS_OK;
+}
+
+// Device scratch for the host-buffer calls: `rows` rows of `pitch` bytes.
+hrs_status ensure_scratch(hrs_codec* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return HRS_OK;
+  if (c->scratch) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->scratch);
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+  }
+  hipError_t e = hipMalloc(&c->scratch, bytes);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  c->scratch_bytes = bytes;
+  return HRS_OK;
+}
+
+size_t pitch_for(size_t len) { return (len + 255) & ~static_cast<size_t>(255); }
+
+// Host rows -> device, apply m, device -> host rows; synchronous.
+hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                      uint8_t* const* out_rows, size_t len, bool static_kp) {
+  if (len == 0 || nout == 0) return HRS_OK;
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  const size_t pitch = pitch_for(len);
+  hrs_status st = ensure_scratch(c, pitch * (nin + nout));
+  if (st != HRS_OK) return st;
+  std::vector<const uint8_t*> din(nin, nullptr);
+  std::vector<uint8_t*> dout(nout);
+  for (int i = 0; i < nin; ++i) {
+    bool any = false;
+    for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
+    if (!any) continue;
+    if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
+    uint8_t* d = c->scratch + pitch * i;
+    hipError_t e = hipMemcpyAsync(d, in_rows[i], len, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
+    din[i] = d;
+  }
+  for (int o = 0; o < nout; ++o) {
+    if (!out_rows[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+    dout[o] = c->scratch + pitch * (nin + o);
+  }
+  st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, c->stream, static_kp);
+  if (st != HRS_OK) return st;
+  for (int o = 0; o < nout; ++o) {
+    hipError_t e = hipMemcpyAsync(out_rows[o], dout[o], len, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+  }
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hipStreamSynchronize");
+  return HRS_OK;
+}
+
+bool sorted_unique_ok(const int* v, int nv, int n) {
+  for (int i = 0; i < nv; ++i)
+    if (v[i] < 0 || v[i] >= n) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hrs_version(void) { return "hrs 0.1.0 (gfx950)"; }
+
+hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out) {
+  if (!out) return fail(nullptr, HRS_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (stripe_size < 1 || parity_size < 1 || stripe_size + parity_size >= gf::kFieldSize ||
+      parity_size > gf::kMaxParity)
+    return fail(nullptr, HRS_EINVAL, "unsupported RS(%d,%d): need k>=1, 1<=p<=%d, k+p<256", stripe_size,
+                parity_size, gf::kMaxParity);
+  if (opts)
+    for (int r : opts->reserved)
+      if (r != 0) return fail(nullptr, HRS_EINVAL, "hrs_opts.reserved must be zero");
+  int dev = opts ? opts->device : -1;
+  if (dev == HRS_DEVICE_NONE) {  // host-only handle: matrices and locations, no coding
+    auto* c = new hrs_codec();
+    c->k = stripe_size;
+    c->p = parity_size;
+    c->n = stripe_size + parity_size;
+    c->device = HRS_DEVICE_NONE;
+    c->g.resize(static_cast<size_t>(parity_size) * stripe_size);
+    gf::encode_matrix(stripe_size, parity_size, c->g.data());
+    *out = c;
+    return HRS_OK;
+  }
+  if (dev < 0) {
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail(nullptr, HRS_EDEVICE, "hipGetDevice: %s", hipGetErrorString(e));
+  }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || dev >= ndev)
+    return fail(nullptr, HRS_EDEVICE, "no HIP device %d (%s)", dev, hipGetErrorString(e));
+  auto* c = new hrs_codec();
+  c->k = stripe_size;
+  c->p = parity_size;
+  c->n = stripe_size + parity_size;
+  c->device = dev;
+  c->g.resize(static_cast<size_t>(parity_size) * stripe_size);
+  gf::encode_matrix(stripe_size, parity_size, c->g.data());
+  {
+    DeviceGuard g(dev);
+    e = g.ok ? hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) : hipErrorInvalidDevice;
+  }
+  if (e != hipSuccess) {
+    delete c;
+    return fail(nullptr, HRS_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return HRS_OK;
+}
+
+void hrs_destroy(hrs_codec* c) {
+  if (!c) return;
+  if (c->device == HRS_DEVICE_NONE) {
+    delete c;
+    return;
+  }
+  DeviceGuard g(c->device);
+  if (c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  if (c->scratch) (void)hipFree(c->scratch);
+  delete c;
+}
+
+const char* hrs_last_error(const hrs_codec* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+int hrs_stripe_size(const hrs_codec* c) { return c ? c->k : -1; }
+int hrs_parity_size(const hrs_codec* c) { return c ? c->p : -1; }
+int hrs_symbol_size(const hrs_codec* c) { return c ? 8 : -1; }  // log2(256), ReedSolomonCode.java:223-226
+
+hrs_status hrs_set_kernel_mode(hrs_codec* c, int mode) {
+  if (!c || mode < 0 || mode > 2) return HRS_EINVAL;
+  c->kernel_mode = mode;
+  return HRS_OK;
+}
+
+hrs_status hrs_locations_to_read(const hrs_codec* cc, const int* erased, int num_erased, int* to_read) {
+  auto* c = const_cast<hrs_codec*>(cc);
+  if (!c || !to_read || num_erased < 0 || (num_erased > 0 && !erased)) return HRS_EINVAL;
+  // ErasureCode.java:89-113: scan locations from the top, keep the first k good ones.
+  int got = 0;
+  for (int loc = c->n - 1; loc >= 0 && got < c->k; --loc) {
+    bool bad = false;
+    for (int i = 0; i < num_erased; ++i) bad |= erased[i] == loc;
+    if (!bad) to_read[got++] = loc;
+  }
+  if (got != c->k) {
+    std::string s = "Locations ";
+    for (int i = 0; i < num_erased; ++i) s += " " + std::to_string(erased[i]);
+    return fail(c, HRS_ETOOMANY, "%s", s.c_str());
+  }
+  return HRS_OK;
+}
+
+hrs_status hrs_encode_matrix(const hrs_codec* c, uint8_t* g) {
+  if (!c || !g) return HRS_EINVAL;
+  std::memcpy(g, c->g.data(), c->g.size());
+  return HRS_OK;
+}
+
+hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, const int* ntr, int nn, int zero_ntr,
+                             uint8_t* d) {
+  auto* c = const_cast<hrs_codec*>(cc);
+  if (!c || !d || ne < 0 || nn < 0 || (ne && !erased) || (nn && !ntr)) return HRS_EINVAL;
+  std::vector<uint8_t> m;
+  hrs_status st = build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, m);
+  if (st == HRS_OK && !m.empty()) std::memcpy(d, m.data(), m.size());
+  return st;
+}
+
+hrs_status hrs_encode(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  if (!c) return HRS_EINVAL;
+  if (!inputs || !outputs) return fail(c, HRS_EINVAL, "inputs/outputs is NULL");
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, true);
+}
+
+hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                      int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len) {
+  if (!c) return HRS_EINVAL;
+  (void)to_read;
+  if (!read_bufs || (ne > 0 && (!write_bufs || !erased)) || ne < 0 || nn < 0 || nr < 0 || (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) || (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+    return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
+  // The Java sizes errSignature by p (ReedSolomonCode.java:60): more than p
+  // not-to-read locations throw there.
+  if (nn > c->p) return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
+  hrs_status st;
+  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, ntr, nn, 1, &st);
+  if (!d) return st;
+  return host_apply(c, d->data(), ne, c->n, read_bufs, write_bufs, len, false);
+}
+
+hrs_status hrs_decode3(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                       int ne, size_t len) {
+  if (!c) return HRS_EINVAL;
+  if (ne < 0 || (ne > 0 && (!read_bufs || !write_bufs || !erased))) return fail(c, HRS_EINVAL, "bad decode3 arguments");
+  if (ne == 0) return HRS_OK;  // ReedSolomonCode.java:170-172
+  if (ne > c->p) return fail(c, HRS_EINVAL, "%d erasures > parity size %d", ne, c->p);  // errSignature[p]
+  hrs_status st;
+  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, erased, ne, 0, &st);
+  if (!d) return st;
+  return host_apply(c, d->data(), ne, c->n, read_bufs, write_bufs, len, false);
+}
+
+hrs_status hrs_encode_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
+                          size_t out_stride, size_t len, size_t nstripes, void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!in_rows || !out_rows) return fail(c, HRS_EINVAL, "row arrays are NULL");
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  return run_apply(c, c->g.data(), c->p, c->k, in_rows, in_stride, out_rows, out_stride, len, nstripes,
+                   static_cast<hipStream_t>(stream), true);
+}
+
+hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_stride, uint8_t* const* out_rows,
+                          size_t out_stride, const int* erased, int ne, const int* ntr, int nn, size_t len,
+                          size_t nstripes, void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!rows || ne < 0 || nn < 0 || (ne > 0 && (!out_rows || !erased)) || (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (nn > c->p) return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
+  hrs_status st;
+  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, ntr, nn, 1, &st);
+  if (!d) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  return run_apply(c, d->data(), ne, c->n, rows, in_stride, out_rows, out_stride, len, nstripes,
+                   static_cast<hipStream_t>(stream), false);
+}
+
+hrs_status hrs_apply_dev(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                         size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
+                         void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!m || !in_rows || !out_rows || nout < 1 || nin < 1 || nout > 255 || nin > 255)
+    return fail(c, HRS_EINVAL, "bad apply arguments");
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  return run_apply(c, m, nout, nin, in_rows, in_stride, out_rows, out_stride, len, nstripes,
+                   static_cast<hipStream_t>(stream), false);
+}
+
+}  // extern "C"

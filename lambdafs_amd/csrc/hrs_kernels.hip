@@ -1,0 +1,349 @@
+// gfx950 kernels of the Reed-Solomon engine.
+//
+// The reference computes parity with a bulk polynomial remainder
+// (GaloisField.java:326-338, driven by ReedSolomonCode.encodeBulk,
+// ReedSolomonCode.java:103-125) and repairs with per-byte syndromes plus a
+// Vandermonde solve (ReedSolomonCode.java:127-166, 191-211). Both are
+// GF(2^8)-linear in the stripe bytes, so every kernel here evaluates
+//     out_o[col] = XOR_i  M[o][i] * in_i[col]        (GF(2^8) products)
+// for every byte column `col` of every stripe, with M = the encode matrix G
+// or a decode matrix D built on the host (hrs_api.cpp).
+//
+// Design (MI355X_MICROARCH.md: HBM ~6.3 TB/s achievable, VALU 64 lanes x 4
+// SIMD x 256 CU): the path is HBM-bound byte streaming, so there is no MFMA
+// here. A GF(2^8) multiply-by-constant is an 8x8 bit matrix over GF(2), so
+// each lane bit-slices 32 bytes of a row into 8 bit-planes (3 exchange stages,
+// 60 VALU ops per 32 B) and then a product becomes plain XORs of planes:
+//   - static kernels: the encode matrix is a compile-time constant, each
+//     output plane is an unrolled XOR of the input planes its bit matrix
+//     selects (~32 XORs per coefficient per 32 B, fused into v_bitop3/xor3);
+//   - runtime kernels: per input row the planes are multiplied by alpha
+//     (a relabelling plus 3 XORs in the sliced domain) and accumulated into
+//     the outputs whose coefficient has that bit set (wave-uniform branches).
+// The bit-slice transform is an involution, applied again to the outputs.
+#include <hip/hip_runtime.h>
+
+#include "gf256.hpp"
+#include "hrs_internal.hpp"
+
+namespace hrs {
+namespace {
+
+// ---------------------------------------------------------------- helpers
+
+__constant__ gf::Tables d_tables = gf::make_tables();
+
+// Three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Bitwise select m ? x : y in one VALU op (v_bitop3_b32, truth table 0xCA).
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
+  return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
+}
+
+// One delta-swap stage between two words: the bits of `a` at positions
+// (M << SH) trade places with the bits of `b` at positions M. Two shifts +
+// two selects = 4 VALU ops.
+template <int SH, uint32_t M>
+__device__ __forceinline__ void xchg(uint32_t& a, uint32_t& b) {
+  const uint32_t na = bsel(M << SH, b << SH, a);
+  const uint32_t nb = bsel(M, a >> SH, b);
+  a = na;
+  b = nb;
+}
+
+// Swap the 3 word-index bits with the 3 bit-in-byte bits of 8 words. Word w,
+// byte j, bit i  <->  word i, byte j, bit w. Afterwards w[i] holds bit i of
+// all 32 bytes (a bit-plane). Involution: applying it twice is the identity.
+__device__ __forceinline__ void bitslice(uint32_t (&w)[8]) {
+  xchg<1, 0x55555555u>(w[0], w[1]);
+  xchg<1, 0x55555555u>(w[2], w[3]);
+  xchg<1, 0x55555555u>(w[4], w[5]);
+  xchg<1, 0x55555555u>(w[6], w[7]);
+  xchg<2, 0x33333333u>(w[0], w[2]);
+  xchg<2, 0x33333333u>(w[1], w[3]);
+  xchg<2, 0x33333333u>(w[4], w[6]);
+  xchg<2, 0x33333333u>(w[5], w[7]);
+  xchg<4, 0x0F0F0F0Fu>(w[0], w[4]);
+  xchg<4, 0x0F0F0F0Fu>(w[1], w[5]);
+  xchg<4, 0x0F0F0F0Fu>(w[2], w[6]);
+  xchg<4, 0x0F0F0F0Fu>(w[3], w[7]);
+}
+
+// Multiply 32 sliced bytes by alpha = 2 modulo 0x11D (x^8 = x^4+x^3+x^2+1).
+__device__ __forceinline__ void xtime(uint32_t (&p)[8]) {
+  const uint32_t hi = p[7];
+  p[7] = p[6];
+  p[6] = p[5];
+  p[5] = p[4];
+  p[4] = p[3] ^ hi;
+  p[3] = p[2] ^ hi;
+  p[2] = p[1] ^ hi;
+  p[1] = p[0];
+  p[0] = hi;
+}
+
+// Lane `lane` of the wave owns bytes [lane*16, +16) and [1024 + lane*16, +16)
+// of the 2 KiB window at `p`. Only whole windows reach these kernels; the
+// row tail (len % 2 KiB) goes to the byte-granular kernel.
+__device__ __forceinline__ void load_row(const uint8_t* p, int lane, uint32_t (&w)[8]) {
+  const uint4 x = *reinterpret_cast<const uint4*>(p + lane * 16);
+  const uint4 y = *reinterpret_cast<const uint4*>(p + 1024 + lane * 16);
+  w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+  w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+}
+
+__device__ __forceinline__ void store_row(uint8_t* p, int lane, const uint32_t (&w)[8]) {
+  *reinterpret_cast<uint4*>(p + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  *reinterpret_cast<uint4*>(p + 1024 + lane * 16) = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+__device__ __forceinline__ uint32_t wave_id_in_grid() {
+  return __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+}
+
+// ------------------------------------------------- static encode kernels
+
+// mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of
+// parity row o (gf::row_mask of G[o][r]). Evaluated by the compiler.
+template <int K, int P>
+struct StaticPlan {
+  uint8_t mask[P][K][8];
+  constexpr StaticPlan() : mask{} {
+    const gf::EncodeMatrix<K, P> g;
+    for (int o = 0; o < P; ++o)
+      for (int r = 0; r < K; ++r)
+        for (int q = 0; q < 8; ++q) mask[o][r][q] = gf::row_mask(g.m[o][r], q);
+  }
+};
+
+template <int K, int P>
+__global__ void __launch_bounds__(kBlockThreads) encode_static_kernel(const RowArgs a) {
+  constexpr StaticPlan<K, P> plan{};
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    uint32_t acc[P][8];
+    uint32_t pend[P][8];
+    bool has[P][8];  // compile-time after unrolling
+#pragma unroll
+    for (int o = 0; o < P; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc[o][q] = 0u;
+        pend[o][q] = 0u;
+        has[o][q] = false;
+      }
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      uint32_t w[8];
+      load_row(a.in[r] + stripe * a.in_stride + off, lane, w);
+      bitslice(w);
+      // acc[o][q] ^= XOR of the planes plan.mask[o][r][q] selects, two
+      // planes per v_bitop3; an odd plane waits in pend for the next row.
+#pragma unroll
+      for (int o = 0; o < P; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if ((plan.mask[o][r][q] >> i) & 1) {
+              if (has[o][q]) {
+                acc[o][q] = xor3(acc[o][q], pend[o][q], w[i]);
+                has[o][q] = false;
+              } else {
+                pend[o][q] = w[i];
+                has[o][q] = true;
+              }
+            }
+          }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < P; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (has[o][q]) acc[o][q] ^= pend[o][q];
+#pragma unroll
+    for (int o = 0; o < P; ++o) {
+      bitslice(acc[o]);
+      store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+  }
+}
+
+// ------------------------------------------ runtime-matrix bit-sliced kernel
+
+template <int NOUT>
+__global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t acc[NOUT][8];
+    if (a.accumulate) {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) {
+        load_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+        bitslice(acc[o]);
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+    }
+    uint32_t cur[8];
+    load_row(a.in[0] + in_base, lane, cur);
+    for (int r = 0; r < a.nin; ++r) {
+      uint32_t nxt[8];
+      if (r + 1 < a.nin) load_row(a.in[r + 1] + in_base, lane, nxt);
+      bitslice(cur);
+      uint32_t c[NOUT];
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) c[o] = a.coef[o][r];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) {
+          if ((c[o] >> b) & 1u) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[o][q] ^= cur[q];
+          }
+        }
+        if (b < 7) xtime(cur);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    }
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      bitslice(acc[o]);
+      store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+  }
+}
+
+// --------------------------------------------- byte-granular kernel (any alignment)
+
+// One byte column per lane, log/antilog tables in LDS. Serves rows that are
+// not 16-byte aligned; ntasks = nstripes * len here.
+__global__ void __launch_bounds__(kBlockThreads) bytewise_kernel(const RowArgs a) {
+  __shared__ uint8_t s_exp[512];
+  __shared__ uint8_t s_log[256];
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) s_exp[i] = d_tables.exp[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_log[i] = d_tables.log[i];
+  __syncthreads();
+  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t idx = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; idx < a.ntasks;
+       idx += nthreads) {
+    const uint64_t stripe = idx / a.len;
+    const uint64_t col = idx - stripe * a.len;
+    uint8_t acc[kMaxOut];
+#pragma unroll
+    for (int o = 0; o < kMaxOut; ++o)
+      acc[o] = (a.accumulate && o < a.nout) ? a.out[o][stripe * a.out_stride + col] : 0;
+    for (int r = 0; r < a.nin; ++r) {
+      const uint8_t x = a.in[r][stripe * a.in_stride + col];
+      if (x == 0) continue;
+      const int lx = s_log[x];
+#pragma unroll
+      for (int o = 0; o < kMaxOut; ++o) {
+        const uint8_t c = a.coef[o][r];
+        if (o < a.nout && c != 0) acc[o] ^= s_exp[lx + s_log[c]];
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < kMaxOut; ++o)
+      if (o < a.nout) a.out[o][stripe * a.out_stride + col] = acc[o];
+  }
+}
+
+// ------------------------------------------------------------ launching
+
+struct DeviceInfo {
+  int cus = 0;
+};
+
+int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  static DeviceInfo infos[64];
+  if (dev < 0 || dev >= 64) return 256;
+  if (infos[dev].cus == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    infos[dev].cus = cus;
+  }
+  return infos[dev].cus;
+}
+
+template <typename Kernel>
+unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t ntasks) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockThreads, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 2;
+  const uint64_t resident = static_cast<uint64_t>(per_cu) * device_cus();
+  const uint64_t needed = (ntasks + work_items_per_block - 1) / work_items_per_block;
+  uint64_t g = needed < resident ? needed : resident;
+  if (g == 0) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+template <int K, int P>
+hipError_t launch_static(const RowArgs& a, hipStream_t s) {
+  auto kern = encode_static_kernel<K, P>;
+  const unsigned g = grid_for(kern, kWavesPerBlock, a.ntasks);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NOUT>
+hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
+  auto kern = bitsliced_kernel<NOUT>;
+  const unsigned g = grid_for(kern, kWavesPerBlock, a.ntasks);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_static_encode(int k, int p, const RowArgs& a, hipStream_t s, bool* handled) {
+  *handled = true;
+  if (k == 10 && p == 4) return launch_static<10, 4>(a, s);
+  if (k == 6 && p == 3) return launch_static<6, 3>(a, s);
+  if (k == 3 && p == 2) return launch_static<3, 2>(a, s);
+  if (k == 12 && p == 4) return launch_static<12, 4>(a, s);
+  *handled = false;
+  return hipSuccess;
+}
+
+hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s) {
+  switch (a.nout) {
+    case 1: return launch_bits<1>(a, s);
+    case 2: return launch_bits<2>(a, s);
+    case 3: return launch_bits<3>(a, s);
+    case 4: return launch_bits<4>(a, s);
+    case 5: return launch_bits<5>(a, s);
+    case 6: return launch_bits<6>(a, s);
+    case 7: return launch_bits<7>(a, s);
+    case 8: return launch_bits<8>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_bytewise(const RowArgs& a, hipStream_t s) {
+  const unsigned g = grid_for(bytewise_kernel, kBlockThreads, a.ntasks);
+  hipLaunchKernelGGL(bytewise_kernel, dim3(g), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hrs

@@ -1,0 +1,89 @@
+"""Device-resident stripe batches on MI355X (the hot path of bench.py).
+
+HBM layout: a batch of S stripes is one uint8 tensor `stripes[S, n, L]` in
+hops location order — rows [0, p) parity, [p, p+k) data — i.e. exactly the
+`data` array ReedSolomonCode.encodeBulk assembles per call
+(ReedSolomonCode.java:114-121), with S stripes stacked. A row view
+`stripes[:, loc, :]` is handed to libhrs as (pointer of stripe 0, stride n*L).
+Decode outputs go to a separate `out[S, e, L]` tensor.
+
+All calls are asynchronous on the current torch stream of the tensors' device.
+"""
+import numpy as np
+
+from . import _lib
+from ._lib import int_array, ptr_array
+
+
+def _rows(views):
+    """[S, L] row views -> (pointer array, stride bytes, L, S)."""
+    if not views:
+        raise ValueError("no rows")
+    strides, shapes = set(), set()
+    for v in views:
+        if v is None:
+            continue
+        if v.dtype != _lib.torch.uint8 or v.dim() != 2 or v.stride(1) != 1 or not v.is_cuda:
+            raise ValueError("row views must be [S, L] uint8 device tensors with unit byte stride")
+        strides.add(v.stride(0) if v.shape[0] > 1 else None)
+        shapes.add(tuple(v.shape))
+    if len(shapes) != 1:
+        raise ValueError("row views differ in shape")
+    strides.discard(None)
+    if len(strides) > 1:
+        raise ValueError("row views differ in stripe stride")
+    S, L = shapes.pop()
+    stride = strides.pop() if strides else L
+    ptrs = ptr_array([None if v is None else v.data_ptr() for v in views])
+    return ptrs, stride, L, S
+
+
+def _stream(t):
+    return _lib.torch.cuda.current_stream(t.device).cuda_stream
+
+
+def encode_stripes(code, stripes):
+    """Parity rows of every stripe from its data rows (encodeBulk over S stripes)."""
+    k, p = code.stripeSize(), code.paritySize()
+    if stripes.dim() != 3 or stripes.shape[1] != k + p:
+        raise ValueError(f"stripes must be [S, {k + p}, L]")
+    ins, s_in, L, S = _rows([stripes[:, p + c, :] for c in range(k)])
+    outs, s_out, _, _ = _rows([stripes[:, r, :] for r in range(p)])
+    code._check(_lib.lib().hrs_encode_dev(code._handle(), ins, s_in, outs, s_out, L, S, _stream(stripes)))
+
+
+def encode_rows(code, data_rows, parity_rows):
+    """encodeBulk with explicit [S, L] row views (k data, p parity)."""
+    ins, s_in, L, S = _rows(data_rows)
+    outs, s_out, L2, S2 = _rows(parity_rows)
+    if (L, S) != (L2, S2):
+        raise ValueError("data and parity views differ in shape")
+    code._check(_lib.lib().hrs_encode_dev(code._handle(), ins, s_in, outs, s_out, L, S, _stream(data_rows[0])))
+
+
+def decode_stripes(code, stripes, erased, not_to_read, out):
+    """decodeBulk 5-arg over S stripes: out[S, e, L] <- the erased locations.
+    Rows of `stripes` at not_to_read locations are never read."""
+    n = code.stripeSize() + code.paritySize()
+    if stripes.dim() != 3 or stripes.shape[1] != n:
+        raise ValueError(f"stripes must be [S, {n}, L]")
+    ntr = set(not_to_read)
+    rows, s_in, L, S = _rows([None if loc in ntr else stripes[:, loc, :] for loc in range(n)])
+    outs, s_out, L2, S2 = _rows([out[:, i, :] for i in range(len(erased))])
+    if (L, S) != (L2, S2):
+        raise ValueError("out must be [S, e, L]")
+    code._check(_lib.lib().hrs_decode_dev(
+        code._handle(), rows, s_in, outs, s_out, int_array(erased), len(erased),
+        int_array(not_to_read), len(not_to_read), L, S, _stream(stripes)))
+
+
+def apply_rows(code, matrix, in_rows, out_rows):
+    """out_o = XOR_i matrix[o, i] * in_i over S stripes (matrix: host uint8 [nout, nin]).
+    Used with coding matrices broadcast over RCCL (bench.py --gpus N)."""
+    m = np.ascontiguousarray(np.asarray(matrix, dtype=np.uint8))
+    ins, s_in, L, S = _rows(in_rows)
+    outs, s_out, L2, S2 = _rows(out_rows)
+    if m.shape != (len(out_rows), len(in_rows)) or (L, S) != (L2, S2):
+        raise ValueError("shape mismatch")
+    code._check(_lib.lib().hrs_apply_dev(code._handle(), m.ctypes.data, m.shape[0], m.shape[1], ins, s_in, outs,
+                                         s_out, L, S, _stream(in_rows[0])))

@@ -1,0 +1,340 @@
+"""Host-side mirror of the hops codec plugin surface, backed by the HIP engine.
+
+`ErasureCode` mirrors io.hops.erasure_coding.ErasureCode
+(hadoop-hdfs-project/hadoop-hdfs/src/main/java/io/hops/erasure_coding/
+ErasureCode.java:25-182) — same method names, argument meaning and error
+behaviour — and `HipReedSolomonCode` is the drop-in for the `rs` codec's
+ReedSolomonCode (hops-erasure-coding/src/main/java/io/hops/erasure_coding/
+ReedSolomonCode.java), computing every byte on the GPU through libhrs.so.
+
+Rows ("byte[][]") may be host buffers (bytearray, writable memoryview,
+contiguous numpy uint8 arrays; read-only `bytes` for inputs) or 1-D uint8
+torch tensors on a HIP device (then the device-resident entry points run).
+"""
+import abc
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, int_array, ptr_array
+
+
+class TooManyErasedLocations(IOError):
+    """io.hops.erasure_coding.TooManyErasedLocations (TooManyErasedLocations.java:26-31)."""
+
+
+class ErasureCode(abc.ABC):
+    """io.hops.erasure_coding.ErasureCode (ErasureCode.java:25-182)."""
+
+    @abc.abstractmethod
+    def encode(self, message, parity):
+        """ErasureCode.java:38 — message: k ints, parity (out): p ints."""
+
+    @abc.abstractmethod
+    def decode(self, data, erasedLocations, erasedValues, locationsToRead=None, locationsNotToRead=None):
+        """ErasureCode.java:55 (3-arg) and :75 (5-arg)."""
+
+    def locationsToReadForDecode(self, erasedLocations):
+        """ErasureCode.java:89-113: the k highest-index locations not erased,
+        highest first; TooManyErasedLocations if fewer than k survive."""
+        locationsToRead = []
+        limit = self.stripeSize() + self.paritySize()
+        for loc in range(limit - 1, -1, -1):
+            if loc not in erasedLocations:
+                locationsToRead.append(loc)
+                if self.stripeSize() == len(locationsToRead):
+                    break
+        if len(locationsToRead) != self.stripeSize():
+            raise TooManyErasedLocations(
+                "Locations " + "".join(" " + str(e) for e in erasedLocations))
+        return locationsToRead
+
+    @abc.abstractmethod
+    def stripeSize(self):
+        ...
+
+    @abc.abstractmethod
+    def paritySize(self):
+        ...
+
+    @abc.abstractmethod
+    def init(self, codec):
+        ...
+
+    @abc.abstractmethod
+    def symbolSize(self):
+        ...
+
+    @abc.abstractmethod
+    def encodeBulk(self, inputs, outputs):
+        """ErasureCode.java:136-156."""
+
+    @abc.abstractmethod
+    def decodeBulk(self, readBufs, writeBufs, erasedLocations, locationsToRead=None, locationsNotToRead=None):
+        """ErasureCode.java:162-181."""
+
+
+# ------------------------------------------------------------------ buffers
+
+def _is_device_tensor(x):
+    t = _lib.torch
+    return t is not None and isinstance(x, t.Tensor) and x.is_cuda
+
+
+def _host_view(buf, writable):
+    if isinstance(buf, np.ndarray):
+        arr = buf
+        if arr.dtype != np.uint8 or arr.ndim != 1 or not arr.flags["C_CONTIGUOUS"]:
+            raise ValueError("host rows must be 1-D contiguous uint8 arrays")
+        if writable and not arr.flags["WRITEABLE"]:
+            raise ValueError("output row is read-only")
+        return arr
+    if isinstance(buf, bytes):
+        if writable:
+            raise ValueError("output row is immutable bytes")
+        return np.frombuffer(buf, dtype=np.uint8)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    if writable and not arr.flags["WRITEABLE"]:
+        raise ValueError("output row is read-only")
+    return arr
+
+
+class _Rows:
+    """Pointers to a byte[][] argument; keeps views alive for the call."""
+
+    def __init__(self, rows, writable, allow_none=False):
+        self.views = []
+        self.device = None
+        ptrs, lens = [], set()
+        for r in rows:
+            if r is None:
+                if not allow_none:
+                    raise ValueError("row is None")
+                ptrs.append(None)
+                self.views.append(None)
+                continue
+            if _is_device_tensor(r):
+                if r.dtype != _lib.torch.uint8 or r.dim() != 1 or not r.is_contiguous():
+                    raise ValueError("device rows must be 1-D contiguous uint8 tensors")
+                dev = r.device.index if r.device.index is not None else 0
+                if self.device not in (None, dev):
+                    raise ValueError("rows span several devices")
+                if self.device is None and len([v for v in self.views if v is not None]) > 0:
+                    raise ValueError("mixed host and device rows")
+                self.device = dev
+                ptrs.append(r.data_ptr())
+                self.views.append(r)
+                lens.add(r.numel())
+            else:
+                if self.device is not None:
+                    raise ValueError("mixed host and device rows")
+                v = _host_view(r, writable)
+                ptrs.append(v.ctypes.data)
+                self.views.append(v)
+                lens.add(v.size)
+        if len(lens) > 1:
+            raise ValueError("rows of different lengths")
+        self.len = lens.pop() if lens else 0
+        self.ptrs = ptr_array(ptrs)
+
+
+# ------------------------------------------------------------ the RS codec
+
+class HipReedSolomonCode(ErasureCode):
+    """Drop-in for ReedSolomonCode (ReedSolomonCode.java:27-308) on MI355X.
+
+    zero_inputs_after_encode: the reference encodeBulk zeroes its `inputs`
+    (the bulk remainder of GaloisField.java:326-338 runs in place);
+    True (default) restores that side effect for host rows.
+    """
+
+    JAVA_CLASS = "io.hops.erasure_coding.HipReedSolomonCode"
+
+    def __init__(self, stripeSize=None, paritySize=None, device=None, zero_inputs_after_encode=True):
+        self._h = None
+        self._k = self._p = 0
+        self._device = device
+        self.zero_inputs_after_encode = zero_inputs_after_encode
+        if stripeSize is not None:
+            self._init(stripeSize, paritySize)
+
+    # -- lifecycle
+    def init(self, codec):
+        """ReedSolomonCode.init(Codec), ReedSolomonCode.java:48-54."""
+        self._init(codec.stripeLength, codec.parityLength)
+
+    def _init(self, k, p):
+        L = _lib.lib()
+        self.close()
+        opts = _lib.HipOpts()
+        opts.device = -1 if self._device is None else int(self._device)
+        h = ctypes.c_void_p()
+        check(L.hrs_create(int(k), int(p), ctypes.byref(opts), ctypes.byref(h)))
+        self._h = h
+        self._k, self._p = int(k), int(p)
+
+    def close(self):
+        if self._h is not None:
+            _lib.lib().hrs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _handle(self):
+        if self._h is None:
+            raise IOError("HipReedSolomonCode used before init()")
+        return self._h
+
+    def _check(self, st):
+        check(st, self._h)
+
+    # -- geometry
+    def stripeSize(self):
+        return self._k
+
+    def paritySize(self):
+        return self._p
+
+    def symbolSize(self):
+        return _lib.lib().hrs_symbol_size(self._handle())
+
+    def setKernelMode(self, mode):
+        """0 auto, 1 runtime-matrix bit-sliced kernel, 2 byte-granular kernel."""
+        self._check(_lib.lib().hrs_set_kernel_mode(self._handle(), int(mode)))
+
+    # -- matrices (host)
+    def encodeMatrix(self):
+        g = np.zeros((self._p, self._k), dtype=np.uint8)
+        self._check(_lib.lib().hrs_encode_matrix(self._handle(), g.ctypes.data))
+        return g
+
+    def decodeMatrix(self, erasedLocations, locationsNotToRead, zero_not_to_read=True):
+        n = self._k + self._p
+        d = np.zeros((max(1, len(erasedLocations)), n), dtype=np.uint8)
+        self._check(_lib.lib().hrs_decode_matrix(
+            self._handle(), int_array(erasedLocations), len(erasedLocations),
+            int_array(locationsNotToRead), len(locationsNotToRead), int(bool(zero_not_to_read)),
+            d.ctypes.data))
+        return d[: len(erasedLocations)]
+
+    # -- bulk (the hot path)
+    def encodeBulk(self, inputs, outputs):
+        """ReedSolomonCode.encodeBulk (ReedSolomonCode.java:103-125)."""
+        if len(inputs) != self._k or len(outputs) != self._p:
+            raise ValueError(f"encodeBulk needs {self._k} inputs and {self._p} outputs")
+        ins = _Rows(inputs, writable=False)
+        outs = _Rows(outputs, writable=True)
+        if ins.len != outs.len:
+            raise ValueError("input and output rows differ in length")
+        L = _lib.lib()
+        if ins.device is not None or outs.device is not None:
+            if ins.device != outs.device:
+                raise ValueError("encodeBulk rows must all be on one device")
+            stream = _lib.torch.cuda.current_stream(ins.device).cuda_stream
+            self._check(L.hrs_encode_dev(self._handle(), ins.ptrs, 0, outs.ptrs, 0, ins.len, 1, stream))
+            return
+        self._check(L.hrs_encode(self._handle(), ins.ptrs, outs.ptrs, ins.len))
+        if self.zero_inputs_after_encode:
+            for v in ins.views:
+                if v.flags["WRITEABLE"]:
+                    v[:] = 0
+
+    def decodeBulk(self, readBufs, writeBufs, erasedLocations, locationsToRead=None, locationsNotToRead=None):
+        """5-arg: ReedSolomonCode.decodeBulk (ReedSolomonCode.java:191-211).
+        3-arg (locationsToRead and locationsNotToRead omitted): the RS-specific
+        decodeBulk(readBufs, writeBufs, erasedLocation), :168-185."""
+        n = self._k + self._p
+        if len(readBufs) != n:
+            raise ValueError(f"decodeBulk needs {n} read buffers")
+        if len(writeBufs) != len(erasedLocations):
+            raise ValueError("one write buffer per erased location")
+        L = _lib.lib()
+        three = locationsNotToRead is None
+        if three:
+            if not erasedLocations:
+                return
+            reads = _Rows(readBufs, writable=False)
+            writes = _Rows(writeBufs, writable=True)
+            if reads.device is not None:
+                m = self.decodeMatrix(erasedLocations, erasedLocations, zero_not_to_read=False)
+                self._apply_dev(m, reads, writes)
+                return
+            self._check(L.hrs_decode3(self._handle(), reads.ptrs, writes.ptrs, int_array(erasedLocations),
+                                      len(erasedLocations), reads.len))
+            return
+        if locationsToRead is None:
+            locationsToRead = []
+        ntr = set(locationsNotToRead)
+        reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
+                      writable=False, allow_none=True)
+        writes = _Rows(writeBufs, writable=True)
+        if not erasedLocations:
+            return
+        if reads.device is not None:
+            stream = _lib.torch.cuda.current_stream(reads.device).cuda_stream
+            self._check(L.hrs_decode_dev(
+                self._handle(), reads.ptrs, 0, writes.ptrs, 0, int_array(erasedLocations), len(erasedLocations),
+                int_array(locationsNotToRead), len(locationsNotToRead), reads.len, 1, stream))
+            return
+        self._check(L.hrs_decode(
+            self._handle(), reads.ptrs, writes.ptrs, int_array(erasedLocations), len(erasedLocations),
+            int_array(locationsToRead), len(locationsToRead), int_array(locationsNotToRead),
+            len(locationsNotToRead), reads.len))
+
+    def _apply_dev(self, m, reads, writes):
+        stream = _lib.torch.cuda.current_stream(reads.device).cuda_stream
+        m = np.ascontiguousarray(m, dtype=np.uint8)
+        self._check(_lib.lib().hrs_apply_dev(self._handle(), m.ctypes.data, m.shape[0], m.shape[1], reads.ptrs, 0,
+                                             writes.ptrs, 0, reads.len, 1, stream))
+
+    # -- scalar (one symbol column; still computed by the GPU engine)
+    def encode(self, message, parity):
+        """ReedSolomonCode.encode (ReedSolomonCode.java:84-97)."""
+        if len(message) != self._k or len(parity) != self._p:
+            raise ValueError("message/parity length mismatch")
+        ins = [np.array([_symbol(v)], dtype=np.uint8) for v in message]
+        outs = [np.zeros(1, dtype=np.uint8) for _ in range(self._p)]
+        saved = self.zero_inputs_after_encode
+        self.zero_inputs_after_encode = False
+        try:
+            self.encodeBulk(ins, outs)
+        finally:
+            self.zero_inputs_after_encode = saved
+        for i in range(self._p):
+            parity[i] = int(outs[i][0])
+
+    def decode(self, data, erasedLocations, erasedValues, locationsToRead=None, locationsNotToRead=None):
+        """3-arg ReedSolomonCode.decode (:127-142) or 5-arg (:144-166).
+        Like the Java, zeroes data at the locations treated as erased."""
+        n = self._k + self._p
+        if len(data) != n or len(erasedValues) != len(erasedLocations):
+            raise ValueError("data/erasedValues length mismatch")
+        if locationsNotToRead is None:
+            if not erasedLocations:
+                return
+            ntr = list(erasedLocations)
+            toread = []
+        else:
+            ntr = list(locationsNotToRead)
+            toread = list(locationsToRead or [])
+        for loc in ntr:
+            data[loc] = 0
+        rows = [np.array([_symbol(v)], dtype=np.uint8) for v in data]
+        outs = [np.zeros(1, dtype=np.uint8) for _ in erasedLocations]
+        if not erasedLocations:
+            return
+        self.decodeBulk(rows, outs, list(erasedLocations), toread, ntr)
+        for i in range(len(erasedLocations)):
+            erasedValues[i] = int(outs[i][0])
+
+
+def _symbol(v):
+    v = int(v)
+    if not 0 <= v < 256:
+        raise ValueError(f"symbol {v} outside GF(2^8)")
+    return v

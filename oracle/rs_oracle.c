@@ -1,0 +1,374 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — CPU oracle for the Reed-Solomon hot path.
+ * Restates the reference Java loop for loop (see rs_oracle.h). Used by
+ * tests/ as the parity checker and by bench.py as the timed CPU baseline
+ * ("restated reference CPU path"); never by the product library.
+ *
+ * Reference files (under /root/reference):
+ *   GaloisField.java     hops-erasure-coding-project/hops-erasure-coding/src/main/java/io/hops/erasure_coding/
+ *   ReedSolomonCode.java same directory
+ *   ErasureCode.java     hadoop-hdfs-project/hadoop-hdfs/src/main/java/io/hops/erasure_coding/
+ */
+#include "rs_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#define FIELD 256
+#define PERIOD 255
+#define PRIM_POLY 285
+
+/* GaloisField.java:30-33: int tables, mul/div 256x256 (divTable[*][0] == 0). */
+static int logTable[FIELD];
+static int powTable[FIELD];
+static int mulTable[FIELD][FIELD];
+static int divTable[FIELD][FIELD];
+
+/* GaloisField(int fieldSize, int primitivePolynomial), GaloisField.java:76-119. */
+__attribute__((constructor)) static void gf_init(void) {
+  int value = 1;
+  for (int pow = 0; pow < FIELD - 1; pow++) {
+    powTable[pow] = value;
+    logTable[value] = pow;
+    value = value * 2;
+    if (value >= FIELD) value = value ^ PRIM_POLY;
+  }
+  for (int i = 0; i < FIELD; i++) {
+    for (int j = 0; j < FIELD; j++) {
+      if (i == 0 || j == 0) {
+        mulTable[i][j] = 0;
+        continue;
+      }
+      int z = logTable[i] + logTable[j];
+      z = z >= PERIOD ? z - PERIOD : z;
+      mulTable[i][j] = powTable[z];
+    }
+  }
+  for (int i = 0; i < FIELD; i++) {
+    for (int j = 1; j < FIELD; j++) {
+      if (i == 0) {
+        divTable[i][j] = 0;
+        continue;
+      }
+      int z = logTable[i] - logTable[j];
+      z = z < 0 ? z + PERIOD : z;
+      divTable[i][j] = powTable[z];
+    }
+  }
+}
+
+int orc_gf_mul(int x, int y) { return mulTable[x][y]; }          /* :162-165 */
+int orc_gf_div(int x, int y) { return divTable[x][y]; }          /* :176-179 */
+int orc_gf_log(int x) { return logTable[x]; }
+int orc_gf_pow_table(int i) { return powTable[i]; }
+
+int orc_gf_power(int x, int n) { /* GaloisField.java:190-204 */
+  if (n == 0) return 1;
+  if (x == 0) return 0;
+  x = logTable[x] * n;
+  if (x < PERIOD) return powTable[x];
+  x = x % PERIOD;
+  return powTable[x];
+}
+
+/* GaloisField.java:286-298 */
+void orc_gf_poly_mul(const int* p, int np, const int* q, int nq, int* result) {
+  int len = np + nq - 1;
+  for (int i = 0; i < len; i++) result[i] = 0;
+  for (int i = 0; i < np; i++)
+    for (int j = 0; j < nq; j++) result[i + j] = result[i + j] ^ mulTable[p[i]][q[j]];
+}
+
+/* GaloisField.java:351-364 */
+void orc_gf_poly_add(const int* p, int np, const int* q, int nq, int* result) {
+  int len = np > nq ? np : nq;
+  for (int i = 0; i < len; i++) {
+    if (i < np && i < nq)
+      result[i] = p[i] ^ q[i];
+    else if (i < np)
+      result[i] = p[i];
+    else
+      result[i] = q[i];
+  }
+}
+
+/* GaloisField.java:310-320 (scalar remainder) */
+void orc_gf_remainder(int* dividend, int nd, const int* divisor, int nv) {
+  for (int i = nd - nv; i >= 0; i--) {
+    int ratio = divTable[dividend[i + nv - 1]][divisor[nv - 1]];
+    for (int j = 0; j < nv; j++) {
+      int k = j + i;
+      dividend[k] = dividend[k] ^ mulTable[ratio][divisor[j]];
+    }
+  }
+}
+
+/* GaloisField.java:326-338 (bulk remainder over byte rows) */
+static void gf_remainder_bulk(uint8_t* const* dividend, int nd, const int* divisor, int nv, size_t len) {
+  for (int i = nd - nv; i >= 0; i--) {
+    for (int j = 0; j < nv; j++) {
+      uint8_t* top = dividend[i + nv - 1];
+      uint8_t* dst = dividend[j + i];
+      const int dv = divisor[nv - 1];
+      for (size_t k = 0; k < len; k++) {
+        int ratio = divTable[top[k] & 0x00FF][dv];
+        dst[k] = (uint8_t)((dst[k] & 0x00FF) ^ mulTable[ratio][divisor[j]]);
+      }
+    }
+  }
+}
+
+/* GaloisField.java:375-383 */
+int orc_gf_substitute(const int* p, int np, int x) {
+  int result = 0;
+  int y = 1;
+  for (int i = 0; i < np; i++) {
+    result = result ^ mulTable[p[i]][y];
+    y = mulTable[x][y];
+  }
+  return result;
+}
+
+/* GaloisField.java:396-406 (bulk substitute) */
+static void gf_substitute_bulk(uint8_t* const* p, int np, uint8_t* q, int x, size_t len) {
+  int y = 1;
+  for (int i = 0; i < np; i++) {
+    const uint8_t* pi = p[i];
+    for (size_t j = 0; j < len; j++) {
+      int pij = pi[j] & 0x000000FF;
+      q[j] = (uint8_t)(q[j] ^ mulTable[pij][y]);
+    }
+    y = mulTable[x][y];
+  }
+}
+
+/* GaloisField.java:232-246 */
+void orc_gf_solve_vandermonde(const int* x, int* y, int len) {
+  for (int i = 0; i < len - 1; i++)
+    for (int j = len - 1; j > i; j--) y[j] = y[j] ^ mulTable[x[i]][y[j - 1]];
+  for (int i = len - 1; i >= 0; i--) {
+    for (int j = i + 1; j < len; j++) y[j] = divTable[y[j]][x[j] ^ x[j - i - 1]];
+    for (int j = i; j < len - 1; j++) y[j] = y[j] ^ y[j + 1];
+  }
+}
+
+/* GaloisField.java:251-273 (bulk Vandermonde) */
+static void gf_solve_vandermonde_bulk(const int* x, uint8_t* const* y, int len, size_t data_len) {
+  for (int i = 0; i < len - 1; i++)
+    for (int j = len - 1; j > i; j--)
+      for (size_t k = 0; k < data_len; k++)
+        y[j][k] = (uint8_t)(y[j][k] ^ mulTable[x[i]][y[j - 1][k] & 0x000000FF]);
+  for (int i = len - 1; i >= 0; i--) {
+    for (int j = i + 1; j < len; j++)
+      for (size_t k = 0; k < data_len; k++) y[j][k] = (uint8_t)(divTable[y[j][k] & 0x000000FF][x[j] ^ x[j - i - 1]]);
+    for (int j = i; j < len - 1; j++)
+      for (size_t k = 0; k < data_len; k++) y[j][k] = (uint8_t)(y[j][k] ^ y[j + 1][k]);
+  }
+}
+
+/* GaloisField.java:412-451; matrix row-major height x width */
+void orc_gf_gaussian_elimination(int* m, int height, int width) {
+  int* tmp = (int*)malloc(sizeof(int) * (size_t)width);
+#define M(r, c) m[(r) * width + (c)]
+  for (int i = 0; i < height; i++) {
+    int pivotFound = 0;
+    for (int j = i; j < height; j++) {
+      if (M(i, j) != 0) { /* sic: the reference tests matrix[i][j] and swaps rows i, j */
+        memcpy(tmp, &M(i, 0), sizeof(int) * (size_t)width);
+        memcpy(&M(i, 0), &M(j, 0), sizeof(int) * (size_t)width);
+        memcpy(&M(j, 0), tmp, sizeof(int) * (size_t)width);
+        pivotFound = 1;
+        break;
+      }
+    }
+    if (!pivotFound) continue;
+    int pivot = M(i, i);
+    for (int j = i; j < width; j++) M(i, j) = divTable[M(i, j)][pivot];
+    for (int j = i + 1; j < height; j++) {
+      int lead = M(j, i);
+      for (int k = i; k < width; k++) M(j, k) = M(j, k) ^ mulTable[lead][M(i, k)];
+    }
+  }
+  for (int i = height - 1; i >= 0; i--) {
+    for (int j = 0; j < i; j++) {
+      int lead = M(j, i);
+      for (int k = i; k < width; k++) M(j, k) = M(j, k) ^ mulTable[lead][M(i, k)];
+    }
+  }
+#undef M
+  free(tmp);
+}
+
+/* ---------------------------------------------------------------- RS code */
+
+/* ReedSolomonCode.init(int,int), ReedSolomonCode.java:56-82 */
+int orc_rs_generator(int k, int p, int* gen_out) {
+  if (k + p >= FIELD) return -1;
+  int n = k + p;
+  int* primitivePower = (int*)malloc(sizeof(int) * (size_t)n);
+  for (int i = 0; i < n; i++) primitivePower[i] = orc_gf_power(2, i);
+  int* gen = (int*)malloc(sizeof(int) * (size_t)(p + 1));
+  int* tmp = (int*)malloc(sizeof(int) * (size_t)(p + 1));
+  int glen = 1;
+  gen[0] = 1;
+  int poly[2];
+  for (int i = 0; i < p; i++) {
+    poly[0] = primitivePower[i];
+    poly[1] = 1;
+    orc_gf_poly_mul(gen, glen, poly, 2, tmp);
+    glen += 1;
+    memcpy(gen, tmp, sizeof(int) * (size_t)glen);
+  }
+  memcpy(gen_out, gen, sizeof(int) * (size_t)(p + 1));
+  free(primitivePower);
+  free(gen);
+  free(tmp);
+  return 0;
+}
+
+/* ReedSolomonCode.encode, :84-97 */
+void orc_rs_encode(int k, int p, const int* message, int* parity) {
+  int gen[FIELD];
+  orc_rs_generator(k, p, gen);
+  int* dataBuff = (int*)malloc(sizeof(int) * (size_t)(k + p));
+  for (int i = 0; i < p; i++) dataBuff[i] = 0;
+  for (int i = 0; i < k; i++) dataBuff[i + p] = message[i];
+  orc_gf_remainder(dataBuff, k + p, gen, p + 1);
+  for (int i = 0; i < p; i++) parity[i] = dataBuff[i];
+  free(dataBuff);
+}
+
+/* ReedSolomonCode.encodeBulk, :103-125 */
+void orc_rs_encode_bulk(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  int gen[FIELD];
+  orc_rs_generator(k, p, gen);
+  for (int i = 0; i < p; i++) memset(outputs[i], 0, len);
+  uint8_t** data = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)(k + p));
+  for (int i = 0; i < p; i++) data[i] = outputs[i];
+  for (int i = 0; i < k; i++) data[i + p] = inputs[i];
+  gf_remainder_bulk(data, k + p, gen, p + 1, len);
+  free(data);
+}
+
+/* ReedSolomonCode.decode 3-arg, :127-142 */
+void orc_rs_decode3(int k, int p, int* data, const int* erased, int ne, int* values) {
+  (void)p;
+  if (ne == 0) return;
+  int n = k + p;
+  int* errSignature = (int*)malloc(sizeof(int) * (size_t)ne);
+  for (int i = 0; i < ne; i++) data[erased[i]] = 0;
+  for (int i = 0; i < ne; i++) {
+    errSignature[i] = orc_gf_power(2, erased[i]);  /* primitivePower[erasedLocations[i]] */
+    values[i] = orc_gf_substitute(data, n, orc_gf_power(2, i));
+  }
+  orc_gf_solve_vandermonde(errSignature, values, ne);
+  free(errSignature);
+}
+
+/* ReedSolomonCode.decode 5-arg, :144-166 */
+void orc_rs_decode5(int k, int p, int* data, const int* erased, int ne, int* values, const int* to_read, int nr,
+                    const int* not_to_read, int nn) {
+  (void)to_read;
+  (void)nr;
+  int* recov = (int*)calloc((size_t)(nn > 0 ? nn : 1), sizeof(int));
+  orc_rs_decode3(k, p, data, not_to_read, nn, recov);
+  for (int i = 0; i < ne; i++) {
+    for (int j = 0; j < nn; j++) {
+      if (erased[i] == not_to_read[j]) {
+        values[i] = recov[j];
+        break;
+      }
+    }
+  }
+  free(recov);
+}
+
+/* ReedSolomonCode.decodeBulk 5-arg, :191-211 */
+void orc_rs_decode_bulk5(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                         int ne, const int* to_read, int nr, const int* not_to_read, int nn, size_t len) {
+  int n = k + p;
+  int* tmpInput = (int*)malloc(sizeof(int) * (size_t)n);
+  int* tmpOutput = (int*)malloc(sizeof(int) * (size_t)(ne > 0 ? ne : 1));
+  for (size_t idx = 0; idx < len; idx++) {
+    for (int i = 0; i < ne; i++) tmpOutput[i] = 0;
+    for (int i = 0; i < n; i++) tmpInput[i] = read_bufs[i] ? (read_bufs[i][idx] & 0x000000FF) : 0;
+    orc_rs_decode5(k, p, tmpInput, erased, ne, tmpOutput, to_read, nr, not_to_read, nn);
+    for (int i = 0; i < ne; i++) write_bufs[i][idx] = (uint8_t)tmpOutput[i];
+  }
+  free(tmpInput);
+  free(tmpOutput);
+}
+
+/* ReedSolomonCode.decodeBulk 3-arg, :168-185 */
+void orc_rs_decode_bulk3(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                         int ne, size_t len) {
+  if (ne == 0) return;
+  int n = k + p;
+  for (int i = 0; i < ne; i++) memset(write_bufs[i], 0, len);
+  int* errSignature = (int*)malloc(sizeof(int) * (size_t)ne);
+  for (int i = 0; i < ne; i++) {
+    errSignature[i] = orc_gf_power(2, erased[i]);
+    gf_substitute_bulk(read_bufs, n, write_bufs[i], orc_gf_power(2, i), len);
+  }
+  gf_solve_vandermonde_bulk(errSignature, write_bufs, ne, len);
+  free(errSignature);
+}
+
+/* ErasureCode.locationsToReadForDecode, ErasureCode.java:89-113 */
+int orc_locations_to_read(int k, int p, const int* erased, int ne, int* out) {
+  int limit = k + p;
+  int got = 0;
+  for (int loc = limit - 1; loc >= 0; loc--) {
+    int bad = 0;
+    for (int i = 0; i < ne; i++)
+      if (erased[i] == loc) bad = 1;
+    if (!bad) {
+      out[got++] = loc;
+      if (got == k) break;
+    }
+  }
+  return got;
+}
+
+/* ReedSolomonCode.computeSyndrome, :298-307 */
+static int compute_syndrome(int k, int p, const int* data, int* syndrome) {
+  int corruption = 0;
+  for (int i = 0; i < p; i++) {
+    syndrome[i] = orc_gf_substitute(data, k + p, orc_gf_power(2, i));
+    if (syndrome[i] != 0) corruption = 1;
+  }
+  return !corruption;
+}
+
+/* ReedSolomonCode.computeErrorLocations, :243-287 */
+int orc_rs_compute_error_locations(int k, int p, int* data, int* locations, int* nloc) {
+  int n = k + p;
+  int maxError = p / 2;
+  int* syndrome = (int*)calloc((size_t)p, sizeof(int));
+  *nloc = 0;
+  if (compute_syndrome(k, p, data, syndrome)) {
+    free(syndrome);
+    return 1;
+  }
+  int w = maxError + 1;
+  int* sm = (int*)calloc((size_t)(maxError * w + 1), sizeof(int));
+  for (int i = 0; i < maxError; ++i)
+    for (int j = 0; j < w; ++j) sm[i * w + j] = syndrome[i + j];
+  if (maxError > 0) orc_gf_gaussian_elimination(sm, maxError, w);
+  int* poly = (int*)calloc((size_t)w, sizeof(int));
+  poly[0] = 1;
+  for (int i = 0; i < maxError; ++i) poly[i + 1] = sm[(maxError - 1 - i) * w + maxError];
+  for (int i = 0; i < n; ++i) {
+    int possibleRoot = orc_gf_div(1, orc_gf_power(2, i));
+    if (orc_gf_substitute(poly, w, possibleRoot) == 0) locations[(*nloc)++] = i;
+  }
+  int* vals = (int*)calloc((size_t)(*nloc > 0 ? *nloc : 1), sizeof(int));
+  orc_rs_decode3(k, p, data, locations, *nloc, vals);
+  for (int i = 0; i < *nloc; ++i) data[locations[i]] = vals[i];
+  int ok = compute_syndrome(k, p, data, syndrome);
+  free(vals);
+  free(poly);
+  free(sm);
+  free(syndrome);
+  return ok;
+}

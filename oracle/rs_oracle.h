@@ -1,0 +1,69 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — the CPU oracle. Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library, and only as the
+ * checker / the timed CPU baseline. The product (lambdafs_amd/libhrs.so)
+ * never links or calls it.
+ *
+ * A C restatement of the reference's Java algorithms, loop for loop:
+ *   GaloisField.java      (hops-erasure-coding/src/main/java/io/hops/erasure_coding/)
+ *   ReedSolomonCode.java  (same directory)
+ *   ErasureCode.java      (hadoop-hdfs/src/main/java/io/hops/erasure_coding/)
+ * Parity pinning: the reference ships no golden vectors and cannot run here
+ * (no JDK); see oracle/README.md for how this restatement is pinned.
+ */
+#ifndef RS_ORACLE_H_
+#define RS_ORACLE_H_
+#include <stddef.h>
+#include <stdint.h>
+
+/* GaloisField(256, 285) tables and scalar ops, GaloisField.java:76-204. */
+int orc_gf_mul(int x, int y);
+int orc_gf_div(int x, int y);
+int orc_gf_power(int x, int n);
+int orc_gf_log(int x);
+int orc_gf_pow_table(int i);
+
+/* Polynomial helpers, GaloisField.java:286-320, :351-383. Arrays index = power. */
+void orc_gf_poly_mul(const int* p, int np, const int* q, int nq, int* out /* np+nq-1 */);
+void orc_gf_poly_add(const int* p, int np, const int* q, int nq, int* out /* max(np,nq) */);
+void orc_gf_remainder(int* dividend, int nd, const int* divisor, int nv);
+int orc_gf_substitute(const int* p, int np, int x);
+void orc_gf_solve_vandermonde(const int* x, int* y, int len);
+void orc_gf_gaussian_elimination(int* matrix, int height, int width);
+
+/* ReedSolomonCode.init generating polynomial, ReedSolomonCode.java:56-82.
+ * gen has p+1 entries. Returns 0, or -1 if k+p >= 256. */
+int orc_rs_generator(int k, int p, int* gen);
+
+/* ReedSolomonCode.encode(int[] message, int[] parity), :84-97. */
+void orc_rs_encode(int k, int p, const int* message, int* parity);
+
+/* ReedSolomonCode.encodeBulk(byte[][] inputs, byte[][] outputs), :103-125,
+ * via the bulk GaloisField.remainder, GaloisField.java:326-338.
+ * Like the Java, this ZEROES the input rows. */
+void orc_rs_encode_bulk(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len);
+
+/* ReedSolomonCode.decode 3-arg, :127-142 (modifies data at erased). */
+void orc_rs_decode3(int k, int p, int* data, const int* erased, int ne, int* values);
+
+/* ReedSolomonCode.decode 5-arg, :144-166. */
+void orc_rs_decode5(int k, int p, int* data, const int* erased, int ne, int* values, const int* to_read, int nr,
+                    const int* not_to_read, int nn);
+
+/* ReedSolomonCode.decodeBulk 5-arg, :191-211 (per byte). */
+void orc_rs_decode_bulk5(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                         int ne, const int* to_read, int nr, const int* not_to_read, int nn, size_t len);
+
+/* ReedSolomonCode.decodeBulk 3-arg, :168-185 (bulk syndromes + bulk Vandermonde). */
+void orc_rs_decode_bulk3(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                         int ne, size_t len);
+
+/* ErasureCode.locationsToReadForDecode, ErasureCode.java:89-113. Returns the
+ * count written (k on success, fewer => TooManyErasedLocations). */
+int orc_locations_to_read(int k, int p, const int* erased, int ne, int* out);
+
+/* ReedSolomonCode.computeErrorLocations, :243-287. Returns 1 if resolved;
+ * writes up to n locations (ascending) and their count. */
+int orc_rs_compute_error_locations(int k, int p, int* data, int* locations, int* nloc);
+
+#endif

@@ -1,0 +1,220 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the C oracle (liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, as the checker or the timed CPU baseline. Rows are numpy uint8
+arrays. The C code restates the reference Java loop for loop (rs_oracle.c).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    """Compile oracle/rs_oracle.c with gcc into oracle/liboracle.so."""
+    src = os.path.join(_HERE, "rs_oracle.c")
+    if os.path.exists(_LIB_PATH) and os.path.getmtime(_LIB_PATH) >= max(
+        os.path.getmtime(src), os.path.getmtime(os.path.join(_HERE, "rs_oracle.h"))
+    ):
+        return _LIB_PATH
+    subprocess.check_call(
+        ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-o", _LIB_PATH, src]
+    )
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        I, P = ctypes.c_int, ctypes.c_void_p
+        S = ctypes.c_size_t
+        IP = ctypes.POINTER(ctypes.c_int)
+        PP = ctypes.POINTER(ctypes.c_void_p)
+        sigs = {
+            "orc_gf_mul": ([I, I], I),
+            "orc_gf_div": ([I, I], I),
+            "orc_gf_power": ([I, I], I),
+            "orc_gf_log": ([I], I),
+            "orc_gf_pow_table": ([I], I),
+            "orc_gf_poly_mul": ([IP, I, IP, I, IP], None),
+            "orc_gf_poly_add": ([IP, I, IP, I, IP], None),
+            "orc_gf_remainder": ([IP, I, IP, I], None),
+            "orc_gf_substitute": ([IP, I, I], I),
+            "orc_gf_solve_vandermonde": ([IP, IP, I], None),
+            "orc_gf_gaussian_elimination": ([IP, I, I], None),
+            "orc_rs_generator": ([I, I, IP], I),
+            "orc_rs_encode": ([I, I, IP, IP], None),
+            "orc_rs_encode_bulk": ([I, I, PP, PP, S], None),
+            "orc_rs_decode3": ([I, I, IP, IP, I, IP], None),
+            "orc_rs_decode5": ([I, I, IP, IP, I, IP, IP, I, IP, I], None),
+            "orc_rs_decode_bulk5": ([I, I, PP, PP, IP, I, IP, I, IP, I, S], None),
+            "orc_rs_decode_bulk3": ([I, I, PP, PP, IP, I, S], None),
+            "orc_locations_to_read": ([I, I, IP, I, IP], I),
+            "orc_rs_compute_error_locations": ([I, I, IP, IP, IP], I),
+        }
+        for name, (args, res) in sigs.items():
+            f = getattr(_lib, name)
+            f.argtypes = args
+            f.restype = res
+        del P
+    return _lib
+
+
+def _ints(values):
+    arr = (ctypes.c_int * max(1, len(values)))(*values)
+    return arr
+
+
+def _rowptrs(rows):
+    ptrs = (ctypes.c_void_p * max(1, len(rows)))()
+    for i, r in enumerate(rows):
+        if r is None:
+            ptrs[i] = None
+        else:
+            assert r.dtype == np.uint8 and r.flags["C_CONTIGUOUS"]
+            ptrs[i] = r.ctypes.data
+    return ptrs
+
+
+# --------------------------------------------------------------- GaloisField
+
+def gf_mul(x, y):
+    return lib().orc_gf_mul(x, y)
+
+
+def gf_div(x, y):
+    return lib().orc_gf_div(x, y)
+
+
+def gf_power(x, n):
+    return lib().orc_gf_power(x, n)
+
+
+def poly_mul(p, q):
+    out = _ints([0] * (len(p) + len(q) - 1))
+    lib().orc_gf_poly_mul(_ints(p), len(p), _ints(q), len(q), out)
+    return list(out)[: len(p) + len(q) - 1]
+
+
+def poly_add(p, q):
+    n = max(len(p), len(q))
+    out = _ints([0] * n)
+    lib().orc_gf_poly_add(_ints(p), len(p), _ints(q), len(q), out)
+    return list(out)[:n]
+
+
+def remainder(dividend, divisor):
+    d = _ints(dividend)
+    lib().orc_gf_remainder(d, len(dividend), _ints(divisor), len(divisor))
+    return list(d)[: len(dividend)]
+
+
+def substitute(p, x):
+    return lib().orc_gf_substitute(_ints(p), len(p), x)
+
+
+def solve_vandermonde(x, y):
+    yy = _ints(y)
+    lib().orc_gf_solve_vandermonde(_ints(x), yy, len(y))
+    return list(yy)[: len(y)]
+
+
+def gaussian_elimination(matrix):
+    h, w = len(matrix), len(matrix[0])
+    flat = _ints([v for row in matrix for v in row])
+    lib().orc_gf_gaussian_elimination(flat, h, w)
+    vals = list(flat)
+    return [vals[i * w:(i + 1) * w] for i in range(h)]
+
+
+# ------------------------------------------------------------ ReedSolomonCode
+
+def generator(k, p):
+    out = _ints([0] * (p + 1))
+    assert lib().orc_rs_generator(k, p, out) == 0
+    return list(out)[: p + 1]
+
+
+def encode(k, p, message):
+    par = _ints([0] * p)
+    lib().orc_rs_encode(k, p, _ints(message), par)
+    return list(par)[:p]
+
+
+def encode_bulk(k, p, inputs, zero_inputs_ok=False):
+    """ReedSolomonCode.encodeBulk. Returns the p parity rows. The Java zeroes
+    its inputs; unless zero_inputs_ok, the rows are copied first."""
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    if not zero_inputs_ok:
+        rows = [r.copy() for r in rows]
+    L = rows[0].size
+    outs = [np.zeros(L, dtype=np.uint8) for _ in range(p)]
+    lib().orc_rs_encode_bulk(k, p, _rowptrs(rows), _rowptrs(outs), L)
+    return outs
+
+
+def decode3(k, p, data, erased):
+    d = _ints(data)
+    vals = _ints([0] * len(erased))
+    lib().orc_rs_decode3(k, p, d, _ints(erased), len(erased), vals)
+    return list(vals)[: len(erased)], list(d)[: len(data)]
+
+
+def decode5(k, p, data, erased, to_read, not_to_read):
+    d = _ints(data)
+    vals = _ints([0] * len(erased))
+    lib().orc_rs_decode5(k, p, d, _ints(erased), len(erased), vals, _ints(to_read), len(to_read),
+                         _ints(not_to_read), len(not_to_read))
+    return list(vals)[: len(erased)]
+
+
+def decode_bulk5(k, p, read_bufs, erased, to_read, not_to_read):
+    rows = [None if r is None else np.ascontiguousarray(r, dtype=np.uint8) for r in read_bufs]
+    L = max(r.size for r in rows if r is not None)
+    outs = [np.zeros(L, dtype=np.uint8) for _ in erased]
+    lib().orc_rs_decode_bulk5(k, p, _rowptrs(rows), _rowptrs(outs), _ints(erased), len(erased),
+                              _ints(to_read), len(to_read), _ints(not_to_read), len(not_to_read), L)
+    return outs
+
+
+def decode_bulk3(k, p, read_bufs, erased):
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in read_bufs]
+    L = rows[0].size
+    outs = [np.zeros(L, dtype=np.uint8) for _ in erased]
+    lib().orc_rs_decode_bulk3(k, p, _rowptrs(rows), _rowptrs(outs), _ints(erased), len(erased), L)
+    return outs
+
+
+def locations_to_read(k, p, erased):
+    out = _ints([0] * k)
+    got = lib().orc_locations_to_read(k, p, _ints(erased), len(erased), out)
+    return list(out)[:got] if got == k else None
+
+
+def compute_error_locations(k, p, data):
+    d = _ints(data)
+    locs = _ints([0] * (k + p))
+    nloc = ctypes.c_int(0)
+    ok = lib().orc_rs_compute_error_locations(k, p, d, locs, ctypes.byref(nloc))
+    return bool(ok), set(list(locs)[: nloc.value]), list(d)[: len(data)]
+
+
+# Raw entry points for the CPU baseline (pointer arrays prepared once).
+def encode_bulk_ptrs(k, p, in_ptrs, out_ptrs, L):
+    lib().orc_rs_encode_bulk(k, p, in_ptrs, out_ptrs, L)
+
+
+def decode_bulk5_ptrs(k, p, in_ptrs, out_ptrs, erased, to_read, not_to_read, L):
+    lib().orc_rs_decode_bulk5(k, p, in_ptrs, out_ptrs, _ints(erased), len(erased), _ints(to_read),
+                              len(to_read), _ints(not_to_read), len(not_to_read), L)
+
+
+rowptrs = _rowptrs

@@ -1,0 +1,135 @@
+"""CPU tests of the product boundary: libhrs.so loads, exports every symbol
+include/hrs.h declares, and its host-side logic (encode/decode matrices,
+locationsToReadForDecode, argument and error handling) agrees with the
+oracle. No coding call runs here (no GPU in this container)."""
+import ctypes
+import itertools
+import os
+import re
+
+import numpy as np
+import pytest
+
+from lambdafs_amd import HipReedSolomonCode, HrsError, TooManyErasedLocations, _lib
+from oracle import rs_oracle as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NONE = -2  # HRS_DEVICE_NONE
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "hrs.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hrs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    names = declared_symbols()
+    assert len(names) >= 17
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(_lib.EXPORTS)
+    assert b"gfx950" in _lib.lib().hrs_version()
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    assert b"encode_static_kernel" in blob and b"bitsliced_kernel" in blob
+
+
+@pytest.mark.parametrize("k,p", [(3, 2), (6, 3), (10, 4), (12, 4), (1, 1), (100, 10), (200, 55)])
+def test_encode_matrix_matches_oracle(k, p):
+    code = HipReedSolomonCode(k, p, device=NONE)
+    G = code.encodeMatrix()
+    for c in range(k):
+        unit = [1 if j == c else 0 for j in range(k)]
+        assert list(G[:, c]) == C.encode(k, p, unit)
+
+
+def _probe_decode5(k, p, erased, to_read, ntr):
+    n = k + p
+    D = np.zeros((len(erased), n), dtype=np.uint8)
+    for col in range(n):
+        unit = [1 if j == col else 0 for j in range(n)]
+        D[:, col] = C.decode5(k, p, unit, erased, to_read, ntr)
+    return D
+
+
+@pytest.mark.parametrize("k,p", [(10, 4), (6, 3), (12, 4)])
+def test_decode_matrix_matches_oracle_all_small_patterns(k, p):
+    code = HipReedSolomonCode(k, p, device=NONE)
+    n = k + p
+    for e in range(1, 3):
+        for erased in itertools.combinations(range(n), e):
+            erased = list(erased)
+            to_read = sorted(C.locations_to_read(k, p, erased))
+            ntr = [x for x in range(n) if x not in to_read]
+            assert (code.decodeMatrix(erased, ntr) == _probe_decode5(k, p, erased, to_read, ntr)).all(), erased
+
+
+def test_decode_matrix_odd_semantics():
+    """Reference quirks the matrices must reproduce (ReedSolomonCode.java:144-166):
+    an erased location missing from notToRead decodes to 0, and fewer
+    notToRead locations than p use fewer syndromes."""
+    k, p = 10, 4
+    code = HipReedSolomonCode(k, p, device=NONE)
+    for erased, ntr in [([4], [1, 2]), ([4, 9], [4]), ([0], [0, 13, 7]), ([5], [])]:
+        D = code.decodeMatrix(erased, ntr)
+        assert (D == _probe_decode5(k, p, erased, [], ntr)).all()
+
+
+def test_decode3_matrix_matches_oracle():
+    k, p = 10, 4
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=NONE)
+    for erased in ([4], [1, 5, 7], [0, 3, 9, 13]):
+        D = code.decodeMatrix(erased, erased, zero_not_to_read=False)
+        for col in range(n):
+            rows = [np.full(1, 1 if j == col else 0, dtype=np.uint8) for j in range(n)]
+            out = C.decode_bulk3(k, p, rows, erased)
+            assert list(D[:, col]) == [int(o[0]) for o in out]
+
+
+def test_locations_to_read_matches_java():
+    code = HipReedSolomonCode(10, 4, device=NONE)
+    lib = _lib.lib()
+    for erased in ([7], [], [0, 13], [4, 1, 5, 7]):
+        out = (ctypes.c_int * 10)()
+        assert lib.hrs_locations_to_read(code._h, _lib.int_array(erased), len(erased), out) == 0
+        assert list(out) == C.locations_to_read(10, 4, erased) == code.locationsToReadForDecode(erased)
+    out = (ctypes.c_int * 10)()
+    st = lib.hrs_locations_to_read(code._h, _lib.int_array([0, 1, 2, 3, 4]), 5, out)
+    assert st == _lib.HRS_ETOOMANY
+    assert b"Locations  0 1 2 3 4" in lib.hrs_last_error(code._h)
+    with pytest.raises(TooManyErasedLocations):
+        code.locationsToReadForDecode([0, 1, 2, 3, 4])
+
+
+def test_create_rejects_bad_geometry():
+    for k, p in [(0, 4), (10, 0), (200, 56), (255, 1)]:
+        with pytest.raises(HrsError) as ei:
+            HipReedSolomonCode(k, p, device=NONE)
+        assert ei.value.status == _lib.HRS_EINVAL
+    assert HipReedSolomonCode(254, 1, device=NONE).stripeSize() == 254
+
+
+def test_decode_matrix_rejects_duplicates_and_range():
+    code = HipReedSolomonCode(10, 4, device=NONE)
+    with pytest.raises(HrsError):
+        code.decodeMatrix([4], [4, 4])
+    with pytest.raises(HrsError):
+        code.decodeMatrix([14], [1])
+
+
+def test_host_only_handle_refuses_coding():
+    code = HipReedSolomonCode(3, 2, device=NONE)
+    with pytest.raises(HrsError) as ei:
+        code.encodeBulk([bytes(8)] * 3, [bytearray(8) for _ in range(2)])
+    assert ei.value.status == _lib.HRS_EDEVICE
+
+
+def test_geometry_accessors():
+    code = HipReedSolomonCode(10, 4, device=NONE)
+    assert (code.stripeSize(), code.paritySize(), code.symbolSize()) == (10, 4, 8)

@@ -1,0 +1,279 @@
+"""Pins the CPU oracle (test infrastructure) before anything is checked against it.
+
+1. Two independent transcriptions of the reference Java (C: oracle/rs_oracle.c,
+   Python: oracle/rs_ref.py) agree byte for byte on random inputs.
+2. Both reproduce the committed golden vectors (tests/golden/).
+3. The reference's own property tests hold on the oracle, restated from
+   TestGaloisField.java:45-224 and TestErasureCodes.java:33-271 (seeded here;
+   the reference's are unseeded).
+"""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import rs_oracle as C
+from oracle import rs_ref as R
+from oracle.java_random import JavaRandom, random_bytes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ------------------------------------------------------------ java.util.Random
+
+def test_java_random_known_values():
+    # Published java.util.Random outputs: new Random(42).nextInt() = -1170105035,
+    # nextInt(10) sequence for seed 42 starts 0, 3, 8 ... ; new Random(0).nextInt() = -1155484576.
+    assert JavaRandom(42).nextInt() == -1170105035
+    assert JavaRandom(0).nextInt() == -1155484576
+    r = JavaRandom(42)
+    assert [r.nextInt(10) for _ in range(3)] == [0, 3, 8]
+    # nextBytes consumes one int per 4 bytes, little-endian byte order
+    x = JavaRandom(7).nextInt()
+    b = random_bytes(7, 4)
+    assert int.from_bytes(b, "little", signed=True) == x
+
+
+# ------------------------------------------------------ transcriptions agree
+
+@pytest.mark.parametrize("k,p", [(3, 2), (6, 3), (10, 4), (12, 4), (1, 1), (20, 9)])
+def test_c_and_python_encode_agree(k, p):
+    rng = np.random.default_rng(k * 100 + p)
+    rows = [rng.integers(0, 256, 40, dtype=np.uint8) for _ in range(k)]
+    c = C.encode_bulk(k, p, rows)
+    py = R.ReedSolomonRef(k, p).encode_bulk([bytes(r) for r in rows])
+    assert [bytes(x) for x in c] == py
+    assert C.generator(k, p) == R.ReedSolomonRef(k, p).gen
+
+
+def test_c_and_python_decode_agree_on_non_codewords():
+    rng = np.random.default_rng(5)
+    k, p = 10, 4
+    n = k + p
+    ref = R.ReedSolomonRef(k, p)
+    for _ in range(30):
+        e = int(rng.integers(1, p + 1))
+        erased = sorted(rng.choice(n, e, replace=False).tolist())
+        to_read = sorted(R.locations_to_read_for_decode(k, p, erased))
+        ntr = [x for x in range(n) if x not in to_read]
+        rows = [rng.integers(0, 256, 16, dtype=np.uint8) for _ in range(n)]  # arbitrary, not a codeword
+        c = C.decode_bulk5(k, p, rows, erased, to_read, ntr)
+        py = ref.decode_bulk5([bytes(r) for r in rows], erased, to_read, ntr)
+        assert [bytes(x) for x in c] == py
+        c3 = C.decode_bulk3(k, p, rows, erased)
+        py3 = ref.decode_bulk3([bytes(r) for r in rows], erased)
+        assert [bytes(x) for x in c3] == py3
+
+
+def test_bulk_remainder_zeroes_inputs_like_java():
+    # GaloisField.java:326-338 runs in place: encodeBulk leaves its inputs zeroed.
+    rows = [np.arange(8, dtype=np.uint8) + i for i in range(3)]
+    C.encode_bulk(3, 2, rows, zero_inputs_ok=True)
+    assert all((r == 0).all() for r in rows)
+
+
+# ------------------------------------------------------------- golden vectors
+
+def test_golden_vectors(golden):
+    for cs in golden["cases"]:
+        k, p = cs["k"], cs["p"]
+        data = [np.frombuffer(bytes.fromhex(h), dtype=np.uint8) for h in cs["data_hex"]]
+        par = C.encode_bulk(k, p, data)
+        assert [bytes(x).hex() for x in par] == cs["parity_hex"], cs["name"]
+        assert C.generator(k, p) == cs["generator"]
+        stripe = [bytes.fromhex(h) for h in cs["parity_hex"] + cs["data_hex"]]
+        for d in cs["decodes"]:
+            assert C.locations_to_read(k, p, d["erased"]) == d["locations_to_read"]
+            reads = [np.frombuffer(stripe[i], dtype=np.uint8) if i in d["locations_to_read_array"]
+                     else np.zeros(cs["len"], dtype=np.uint8) for i in range(k + p)]
+            out = C.decode_bulk5(k, p, reads, d["erased"], d["locations_to_read_array"],
+                                 d["locations_not_to_read_array"])
+            assert [bytes(x).hex() for x in out] == d["outputs_hex"]
+
+
+def test_golden_encode_matrix(golden):
+    G = golden["encode_matrix_10_4"]
+    assert G[0] == [64, 231, 229, 158, 164, 178, 132, 140, 113, 34]
+    assert [[C.encode(10, 4, [1 if j == c else 0 for j in range(10)])[r] for c in range(10)]
+            for r in range(4)] == G
+
+
+def test_config1_rs32_1mib_fixture():
+    with open(os.path.join(ROOT, "tests", "golden", "config1_rs_3_2_1mib.json")) as f:
+        cfg = json.load(f)
+    L = cfg["len"]
+    buf = random_bytes(0x5EED0001, 3 * L)
+    assert hashlib.sha256(buf).hexdigest() == cfg["input_sha256"]
+    rows = [np.frombuffer(buf[i * L:(i + 1) * L], dtype=np.uint8) for i in range(3)]
+    par = C.encode_bulk(3, 2, rows)
+    assert [hashlib.sha256(bytes(r)).hexdigest() for r in par] == cfg["parity_sha256"]
+
+
+# ------------------------------------ TestGaloisField.java, restated (seeded)
+
+RAND = random.Random(1234)
+TEST_TIMES = 2000
+
+
+def rand_gf():
+    return RAND.randrange(256)
+
+
+def rand_poly(n):
+    return [rand_gf() for _ in range(n)]
+
+
+def test_gf_distributivity():  # TestGaloisField.java:57-68
+    for _ in range(TEST_TIMES):
+        a, b, c = rand_gf(), rand_gf(), rand_gf()
+        assert C.gf_mul(a, b ^ c) == C.gf_mul(a, b) ^ C.gf_mul(a, c)
+
+
+def test_gf_division():  # :70-81
+    for _ in range(TEST_TIMES):
+        a, b = rand_gf(), rand_gf()
+        if b == 0:
+            continue
+        assert C.gf_mul(C.gf_div(a, b), b) == a
+
+
+def test_gf_power():  # :83-94
+    for _ in range(TEST_TIMES):
+        a, n = rand_gf(), RAND.randrange(10)
+        r = 1
+        for _ in range(n):
+            r = C.gf_mul(r, a)
+        assert C.gf_power(a, n) == r
+
+
+def test_gf_polynomial_distributivity():  # :96-107
+    for _ in range(300):
+        a, b, c = (rand_poly(RAND.randrange(14) + 1) for _ in range(3))
+        assert C.poly_mul(a, C.poly_add(b, c)) == C.poly_add(C.poly_mul(a, b), C.poly_mul(a, c))
+
+
+def test_gf_substitute():  # :109-124
+    for _ in range(300):
+        a, b, c = (rand_poly(RAND.randrange(14) + 1) for _ in range(3))
+        x = rand_gf()
+        lhs = C.substitute(C.poly_mul(C.poly_mul(a, b), c), x)
+        rhs = C.gf_mul(C.gf_mul(C.substitute(a, x), C.substitute(b, x)), C.substitute(c, x))
+        assert lhs == rhs
+
+
+def test_gf_solve_vandermonde():  # :126-154
+    for _ in range(300):
+        z = rand_poly(RAND.randrange(14) + 1)
+        xs = set()
+        while len(xs) != len(z):
+            xs.add(rand_gf())
+        x = list(xs)
+        y = [0] * len(x)
+        for j in range(len(x)):
+            for k in range(len(x)):
+                y[j] ^= C.gf_mul(C.gf_power(x[k], j), z[k])
+        assert C.solve_vandermonde(x, y) == z
+
+
+def test_gf_remainder():  # :156-181
+    for _ in range(300):
+        while True:
+            quotient = rand_poly(RAND.randrange(12) + 3)
+            divisor = rand_poly(RAND.randrange(len(quotient) - 2) + 2)
+            rem = rand_poly(RAND.randrange(len(divisor) - 1) + 1)
+            dividend = C.poly_add(rem, C.poly_mul(quotient, divisor))
+            if quotient[-1] and divisor[-1] and rem[-1]:
+                break
+        out = C.remainder(dividend, divisor)
+        assert out[: len(rem)] == rem
+
+
+def test_gf_gaussian_elimination():  # :183-224
+    checked = 0
+    for _ in range(500):
+        m = [[rand_gf() for _ in range(5)] for _ in range(4)]
+        r = C.gaussian_elimination(m)
+        if any(r[i][i] == 0 for i in range(4)):
+            continue
+        checked += 1
+        for i in range(4):
+            for j in range(5):
+                acc = 0
+                for k in range(4):
+                    acc ^= C.gf_mul(m[i][k], r[k][j])
+                assert acc == m[i][j]
+    assert checked > 100
+
+
+# ----------------------------------- TestErasureCodes.java, restated (seeded)
+
+def test_encode_decode_random_codes():  # TestErasureCodes.java:33-69
+    rnd = random.Random(99)
+    for _ in range(40):
+        k = rnd.randrange(99) + 1
+        p = rnd.randrange(9) + 1
+        for _ in range(10):
+            msg = [rnd.randrange(256) for _ in range(k)]
+            par = C.encode(k, p, msg)
+            data = par + msg
+            copy = list(data)
+            e = 1 if p == 1 else rnd.randrange(p - 1) + 1
+            erased = rnd.sample(range(k + p), e)
+            for loc in erased:
+                data[loc] = 0
+            vals, _ = C.decode3(k, p, data, erased)
+            assert vals == [copy[loc] for loc in erased]
+
+
+@pytest.mark.parametrize("k,p", [(10, 4), (3, 3)])
+def test_rs_encode_decode_bulk(k, p):  # TestErasureCodes.java:139-195 (1 MiB instead of 10 MiB)
+    rng = np.random.default_rng(k)
+    L = 1 << 20
+    msg = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    par = C.encode_bulk(k, p, msg)
+    erased = int(rng.integers(0, k))
+    copy = msg[erased].copy()
+    data = [x.copy() for x in par] + [x.copy() for x in msg]
+    data[erased + p][:] = 0
+    out = C.decode_bulk3(k, p, data, [erased + p])
+    assert (out[0] == copy).all()
+
+
+def test_rs_performance_pattern():  # TestErasureCodes.java:71-137: erasures {4,1,5,7}
+    rng = np.random.default_rng(3)
+    k, p = 10, 4
+    for _ in range(200):
+        msg = [int(v) for v in rng.integers(0, 256, k)]
+        par = C.encode(k, p, msg)
+        data = par + msg
+        vals, _ = C.decode3(k, p, list(data), [4, 1, 5, 7])
+        assert vals[0] == msg[0]
+
+
+def test_compute_error_locations():  # TestErasureCodes.java:242-271
+    rnd = random.Random(11)
+    for errors in (1, 2):
+        for _ in range(200):
+            msg = [rnd.randrange(256) for _ in range(10)]
+            locs = set()
+            while len(locs) < errors:
+                locs.add(rnd.randrange(14))
+            data = C.encode(10, 4, msg) + msg
+            for i in locs:
+                while True:
+                    r = rnd.randrange(256)
+                    if r != data[i]:
+                        data[i] = r
+                        break
+            ok, found, _ = C.compute_error_locations(10, 4, data)
+            if ok:
+                assert found == locs
+
+
+def test_locations_to_read_for_decode():  # ErasureCode.java:89-113
+    assert C.locations_to_read(10, 4, [7]) == [13, 12, 11, 10, 9, 8, 6, 5, 4, 3]
+    assert C.locations_to_read(10, 4, [0, 1, 2, 3, 4]) is None
+    assert R.locations_to_read_for_decode(10, 4, [7]) == C.locations_to_read(10, 4, [7])
