@@ -29,7 +29,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from lambdafs_amd import HipReedSolomonCode, device  # noqa: E402
+from lambdafs_amd import HipReedSolomonCode, device, parallel  # noqa: E402
 
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU")
+    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU (weak scaling)")
+    ap.add_argument("--strong", action="store_true",
+                    help="--stripes is the job total, split into contiguous ranges over the ranks")
     ap.add_argument("--cell", type=int, default=1 << 20, help="cell bytes (bufSize)")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--p", type=int, default=4)
@@ -58,22 +60,6 @@ def setup_dist(args):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
-
-
-def barrier(world):
-    if world > 1:
-        dist.barrier()
-
-
-def broadcast_matrix(m, world, local):
-    """Rank 0's coding matrix over RCCL; every rank checks it against its own."""
-    t = torch.from_numpy(np.ascontiguousarray(m)).to(f"cuda:{local}")
-    if world > 1:
-        dist.broadcast(t, src=0)
-    got = t.cpu().numpy()
-    if not np.array_equal(got, m):
-        raise RuntimeError("broadcast coding matrix differs from the local one")
-    return got
 
 
 def cpu_baseline(k, p, L, nstripes):
@@ -132,23 +118,29 @@ def main():
     world, rank, local = setup_dist(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    k, p, L, S = args.k, args.p, args.cell, args.stripes
+    k, p, L = args.k, args.p, args.cell
+    if args.strong:
+        lo, hi = parallel.stripe_range(args.stripes, world, rank)
+        S = hi - lo
+    else:
+        S = args.stripes
     n = k + p
+    dev = f"cuda:{local}"
     code = HipReedSolomonCode(k, p, device=local)
 
     # coding matrices: built on rank 0, broadcast over RCCL, checked everywhere
     erased = [p]  # data shard 0 = hops location p
     to_read = sorted(code.locationsToReadForDecode(erased))
     ntr = [x for x in range(n) if x not in to_read]
-    G = broadcast_matrix(code.encodeMatrix(), world, local)
-    D = broadcast_matrix(code.decodeMatrix(erased, ntr), world, local)
+    G = parallel.broadcast_matrix(code.encodeMatrix(), dev)
+    D = parallel.broadcast_matrix(code.decodeMatrix(erased, ntr), dev)
     D_live = np.ascontiguousarray(D[:, to_read])
 
     # synthetic stripes, resident in HBM before timing: [S, n, L] hops order
-    gen = torch.Generator(device=f"cuda:{local}")
+    gen = torch.Generator(device=dev)
     gen.manual_seed(0x5EED0003 + rank)
-    stripes = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device=f"cuda:{local}", generator=gen)
-    out = torch.empty((S, len(erased), L), dtype=torch.uint8, device=f"cuda:{local}")
+    stripes = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device=dev, generator=gen)
+    out = torch.empty((S, len(erased), L), dtype=torch.uint8, device=dev)
     in_rows = [stripes[:, loc, :] for loc in to_read]
     out_rows = [out[:, 0, :]]
     assert G.shape == (p, k)
@@ -167,18 +159,14 @@ def main():
         step()
     torch.cuda.synchronize()
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    barrier(world)
+    parallel.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(events[i])
     torch.cuda.synchronize()
-    barrier(world)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    parallel.barrier()
+    elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
@@ -190,13 +178,11 @@ def main():
         host = stripes[S // 2].cpu().numpy()
         ref = np.stack(C.encode_bulk(k, p, [host[p + c] for c in range(k)]))
         ok &= bool((host[:p] == ref).all())
-    okt = torch.tensor([1 if ok else 0], device=f"cuda:{local}")
-    if world > 1:
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    if not bool(okt.item()):
+    if not parallel.all_ok(ok, dev):
         raise RuntimeError("benchmark output failed its round-trip check")
 
-    user_bytes = 2 * k * L * S * world * args.steps
+    total_stripes = args.stripes if args.strong else S * world
+    user_bytes = 2 * k * L * total_stripes * args.steps
     enc_bytes = (k + p) * L * S  # algorithmic bytes per encode launch (read k, write p)
     dec_bytes = (k + len(erased)) * L * S
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
@@ -213,14 +199,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint uniform bytes, seeded per rank)",
             "config": {
                 "workload": f"RS({k},{p}) encode + 1-erasure decode (data shard 0), {L >> 10} KiB cells, "
                             f"{S} stripes/GPU, device-resident",
-                "stripes_per_gpu": S, "cell_bytes": L, "k": k, "p": p,
+                "stripes_per_gpu": S, "stripes_total": total_stripes, "cell_bytes": L, "k": k, "p": p,
                 "parallelism": f"stripe-sharded x{world} (RCCL: matrix broadcast + barriers only)",
             },
             "encode_GiBps_per_gpu": round(k * L * S / GiB / (enc_ms * 1e-3), 3),

@@ -1,0 +1,165 @@
+/*
+ * The Java side of the drop-in: a codec class for the hops erasure-coding
+ * plugin surface (hadoop-hdfs/src/main/java/io/hops/erasure_coding/
+ * ErasureCode.java:25-182), to be added to
+ * hops-erasure-coding-project/hops-erasure-coding/src/main/java/io/hops/erasure_coding/
+ * and selected with  hdfs.raid.erasure.code.rs = io.hops.erasure_coding.HipReedSolomonCode
+ * (Codec.java:52-53, :200-213). Semantics are those of ReedSolomonCode, bit-exact;
+ * every byte is computed by libhrs.so (MI355X) through libhrs_jni.so.
+ *
+ * Not compiled in this repository's CI (no JDK in the build image): see
+ * INTEGRATION.md for the build recipe.
+ */
+package io.hops.erasure_coding;
+
+import java.io.IOException;
+import java.util.Arrays;
+
+public class HipReedSolomonCode extends ErasureCode {
+  static {
+    System.loadLibrary("hrs_jni");  // libhrs_jni.so -> libhrs.so
+  }
+
+  private long nativeCodec;  // hrs_codec*, owned (cf. jni_common.c:35-70 "nativeCoder")
+  private int stripeSize;
+  private int paritySize;
+
+  public HipReedSolomonCode() {
+  }
+
+  @Deprecated
+  public HipReedSolomonCode(int stripeSize, int paritySize) {
+    init(stripeSize, paritySize);
+  }
+
+  @Override
+  public void init(Codec codec) {  // ReedSolomonCode.java:48-54
+    init(codec.stripeLength, codec.parityLength);
+  }
+
+  private synchronized void init(int stripeSize, int paritySize) {
+    release();
+    this.stripeSize = stripeSize;
+    this.paritySize = paritySize;
+    this.nativeCodec = nativeCreate(stripeSize, paritySize);  // throws IllegalArgumentException / RuntimeException
+  }
+
+  /** Same result as ReedSolomonCode.encodeBulk (ReedSolomonCode.java:103-125). */
+  @Override
+  public void encodeBulk(byte[][] inputs, byte[][] outputs) throws IOException {
+    assert (stripeSize == inputs.length);
+    assert (paritySize == outputs.length);
+    nativeEncode(nativeCodec, inputs, outputs, outputs[0].length);
+    // The Java bulk remainder zeroes its inputs (GaloisField.java:326-338); keep that contract.
+    for (byte[] in : inputs) {
+      Arrays.fill(in, (byte) 0);
+    }
+  }
+
+  /** Same result as ReedSolomonCode.decodeBulk 5-arg (ReedSolomonCode.java:191-211). */
+  @Override
+  public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocations,
+      int[] locationsToRead, int[] locationsNotToRead) throws IOException {
+    if (erasedLocations.length == 0) {
+      return;
+    }
+    nativeDecode(nativeCodec, readBufs, writeBufs, erasedLocations, locationsToRead,
+        locationsNotToRead, readBufs[0].length);
+  }
+
+  /** Same result as ReedSolomonCode.decodeBulk 3-arg (ReedSolomonCode.java:168-185). */
+  public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocation)
+      throws IOException {
+    if (erasedLocation.length == 0) {
+      return;
+    }
+    nativeDecode3(nativeCodec, readBufs, writeBufs, erasedLocation, readBufs[0].length);
+  }
+
+  @Override
+  public void encode(int[] message, int[] parity) {  // ReedSolomonCode.java:84-97
+    byte[][] in = new byte[stripeSize][1];
+    byte[][] out = new byte[paritySize][1];
+    for (int i = 0; i < stripeSize; i++) {
+      in[i][0] = (byte) message[i];
+    }
+    try {
+      nativeEncode(nativeCodec, in, out, 1);
+    } catch (IOException e) {
+      throw new RuntimeException(e);
+    }
+    for (int i = 0; i < paritySize; i++) {
+      parity[i] = out[i][0] & 0xFF;
+    }
+  }
+
+  @Override
+  public void decode(int[] data, int[] erasedLocations, int[] erasedValues) {  // :127-142
+    if (erasedLocations.length == 0) {
+      return;
+    }
+    decode(data, erasedLocations, erasedValues, new int[0], erasedLocations);
+  }
+
+  @Override
+  public void decode(int[] data, int[] erasedLocations, int[] erasedValues,
+      int[] locationsToRead, int[] locationsNotToRead) {  // :144-166
+    for (int loc : locationsNotToRead) {
+      data[loc] = 0;  // the Java zeroes data at the decoded locations
+    }
+    byte[][] rows = new byte[data.length][1];
+    for (int i = 0; i < data.length; i++) {
+      rows[i][0] = (byte) data[i];
+    }
+    byte[][] out = new byte[erasedLocations.length][1];
+    try {
+      nativeDecode(nativeCodec, rows, out, erasedLocations, locationsToRead, locationsNotToRead, 1);
+    } catch (IOException e) {
+      throw new RuntimeException(e);
+    }
+    for (int i = 0; i < erasedLocations.length; i++) {
+      erasedValues[i] = out[i][0] & 0xFF;
+    }
+  }
+
+  @Override
+  public int stripeSize() {
+    return stripeSize;
+  }
+
+  @Override
+  public int paritySize() {
+    return paritySize;
+  }
+
+  @Override
+  public int symbolSize() {
+    return 8;
+  }
+
+  public synchronized void release() {
+    if (nativeCodec != 0) {
+      nativeDestroy(nativeCodec);
+      nativeCodec = 0;
+    }
+  }
+
+  @Override
+  protected void finalize() throws Throwable {
+    release();
+    super.finalize();
+  }
+
+  private static native long nativeCreate(int stripeSize, int paritySize);
+
+  private static native void nativeDestroy(long codec);
+
+  private static native void nativeEncode(long codec, byte[][] inputs, byte[][] outputs, int len)
+      throws IOException;
+
+  private static native void nativeDecode(long codec, byte[][] readBufs, byte[][] writeBufs,
+      int[] erased, int[] toRead, int[] notToRead, int len) throws IOException;
+
+  private static native void nativeDecode3(long codec, byte[][] readBufs, byte[][] writeBufs,
+      int[] erased, int len) throws IOException;
+}

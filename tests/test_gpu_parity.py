@@ -105,7 +105,7 @@ def test_unaligned_rows_use_bytewise_kernel(cuda):
     torch = cuda
     k, p, L = 10, 4, 5000
     code = HipReedSolomonCode(k, p)
-    buf = torch.randint(0, 256, (k + p) * (L + 1) + 64, dtype=torch.uint8, device="cuda")
+    buf = torch.randint(0, 256, ((k + p) * (L + 1) + 64,), dtype=torch.uint8, device="cuda")
     data = [buf[1 + i * (L + 1): 1 + i * (L + 1) + L] for i in range(k)]  # odd offsets
     par = [torch.zeros(L + 3, dtype=torch.uint8, device="cuda")[3:] for _ in range(p)]
     code.encodeBulk(data, par)
