@@ -252,8 +252,9 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
   const int nlive = static_cast<int>(live.size());
   for (int o0 = 0; o0 < nout; o0 += hrs::kMaxOut) {
     const int no = std::min(hrs::kMaxOut, nout - o0);
-    for (int i0 = 0; i0 < nlive; i0 += hrs::kMaxIn) {
-      const int ni = std::min(hrs::kMaxIn, nlive - i0);
+    const int chunk = hrs::runtime_in_chunk(no);
+    for (int i0 = 0; i0 < nlive; i0 += chunk) {
+      const int ni = std::min(chunk, nlive - i0);
       RowArgs a{};
       for (int i = 0; i < ni; ++i) a.in[i] = in_rows[live[i0 + i]];
       for (int o = 0; o < no; ++o) {

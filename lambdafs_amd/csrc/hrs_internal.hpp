@@ -10,7 +10,10 @@ namespace hrs {
 // Rows one launch reads / writes. Larger problems are split by the host:
 // inputs in chunks of kMaxIn (later chunks accumulate into the outputs),
 // outputs in chunks of kMaxOut.
-constexpr int kMaxIn = 32;
+constexpr int kMaxIn = 32;         // RowArgs capacity (static kernels: k <= 32)
+constexpr int kMaxInRuntime = 16;  // inputs per runtime-matrix launch (<= 5 outputs)
+constexpr int kMaxInRuntimeWide = 8;  // inputs per launch with 6..8 outputs
+inline int runtime_in_chunk(int nout) { return nout <= 5 ? kMaxInRuntime : kMaxInRuntimeWide; }
 constexpr int kMaxOut = 8;
 
 // One wave owns a 2 KiB column window of every row of one stripe: each lane

@@ -23,6 +23,8 @@
 // The bit-slice transform is an involution, applied again to the outputs.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gf256.hpp"
 #include "hrs_internal.hpp"
 
@@ -87,17 +89,23 @@ __device__ __forceinline__ void xtime(uint32_t (&p)[8]) {
 
 // Lane `lane` of the wave owns bytes [lane*16, +16) and [1024 + lane*16, +16)
 // of the 2 KiB window at `p`. Only whole windows reach these kernels; the
-// row tail (len % 2 KiB) goes to the byte-granular kernel.
+// row tail (len % 2 KiB) goes to the byte-granular kernel. Every byte is
+// touched once, so loads and stores are nontemporal (streaming; measured
+// +4% over default-policy accesses, tools/kernel_lab.hip).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void load_row(const uint8_t* p, int lane, uint32_t (&w)[8]) {
-  const uint4 x = *reinterpret_cast<const uint4*>(p + lane * 16);
-  const uint4 y = *reinterpret_cast<const uint4*>(p + 1024 + lane * 16);
-  w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-  w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + lane * 16));
+  const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 + lane * 16));
+  w[0] = x[0]; w[1] = x[1]; w[2] = x[2]; w[3] = x[3];
+  w[4] = y[0]; w[5] = y[1]; w[6] = y[2]; w[7] = y[3];
 }
 
 __device__ __forceinline__ void store_row(uint8_t* p, int lane, const uint32_t (&w)[8]) {
-  *reinterpret_cast<uint4*>(p + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-  *reinterpret_cast<uint4*>(p + 1024 + lane * 16) = make_uint4(w[4], w[5], w[6], w[7]);
+  const u32x4 x = {w[0], w[1], w[2], w[3]};
+  const u32x4 y = {w[4], w[5], w[6], w[7]};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p + lane * 16));
+  __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(p + 1024 + lane * 16));
 }
 
 __device__ __forceinline__ uint32_t wave_id_in_grid() {
@@ -178,14 +186,22 @@ __global__ void __launch_bounds__(kBlockThreads) encode_static_kernel(const RowA
 
 // ------------------------------------------ runtime-matrix bit-sliced kernel
 
-template <int NOUT>
+// NINB >= nin rows of the window are all loaded before any math (one
+// 20 KiB-class burst per wave, like the static kernel), so a wave keeps
+// nin x 2 KiB in flight; coefficients are wave-uniform kernel arguments.
+template <int NOUT, int NINB>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const int nin = a.nin;
   for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t rows[NINB][8];
+#pragma unroll
+    for (int r = 0; r < NINB; ++r)
+      if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
     uint32_t acc[NOUT][8];
     if (a.accumulate) {
 #pragma unroll
@@ -199,28 +215,25 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
     }
-    uint32_t cur[8];
-    load_row(a.in[0] + in_base, lane, cur);
-    for (int r = 0; r < a.nin; ++r) {
-      uint32_t nxt[8];
-      if (r + 1 < a.nin) load_row(a.in[r + 1] + in_base, lane, nxt);
-      bitslice(cur);
-      uint32_t c[NOUT];
 #pragma unroll
-      for (int o = 0; o < NOUT; ++o) c[o] = a.coef[o][r];
+    for (int r = 0; r < NINB; ++r) {
+      if (r < nin) {
+        bitslice(rows[r]);
+        uint32_t c[NOUT];
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
+        for (int o = 0; o < NOUT; ++o) c[o] = a.coef[o][r];
 #pragma unroll
-        for (int o = 0; o < NOUT; ++o) {
-          if ((c[o] >> b) & 1u) {
+        for (int b = 0; b < 8; ++b) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[o][q] ^= cur[q];
+          for (int o = 0; o < NOUT; ++o) {
+            if ((c[o] >> b) & 1u) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) acc[o][q] ^= rows[r][q];
+            }
           }
+          if (b < 7) xtime(rows[r]);
         }
-        if (b < 7) xtime(cur);
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
     }
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
@@ -285,6 +298,27 @@ int device_cus() {
   return infos[dev].cus;
 }
 
+// Streaming kernels: a fixed number of resident blocks per CU, grid-striding
+// over the tasks. 2 x 256-thread blocks per CU (8 waves, each with a whole
+// window's rows in flight) measured fastest for both the static and the
+// runtime kernels (tools/kernel_lab.hip sweep, 256..1024 blocks); override
+// with HRS_BLOCKS_PER_CU for experiments.
+int blocks_per_cu() {
+  static int v = [] {
+    const char* e = getenv("HRS_BLOCKS_PER_CU");
+    int x = e ? atoi(e) : 0;
+    return (x >= 1 && x <= 32) ? x : 2;
+  }();
+  return v;
+}
+
+unsigned stream_grid(uint64_t ntasks) {
+  const uint64_t want = static_cast<uint64_t>(blocks_per_cu()) * device_cus();
+  const uint64_t needed = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+  uint64_t g = needed < want ? needed : want;
+  return static_cast<unsigned>(g == 0 ? 1 : g);
+}
+
 template <typename Kernel>
 unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t ntasks) {
   int per_cu = 0;
@@ -301,17 +335,27 @@ unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t ntasks)
 template <int K, int P>
 hipError_t launch_static(const RowArgs& a, hipStream_t s) {
   auto kern = encode_static_kernel<K, P>;
-  const unsigned g = grid_for(kern, kWavesPerBlock, a.ntasks);
+  const unsigned g = stream_grid(a.ntasks);
   hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NOUT, int NINB>
+hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
+  auto kern = bitsliced_kernel<NOUT, NINB>;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }
 
 template <int NOUT>
 hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
-  auto kern = bitsliced_kernel<NOUT>;
-  const unsigned g = grid_for(kern, kWavesPerBlock, a.ntasks);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
-  return hipGetLastError();
+  if (a.nin <= 4) return launch_bits_n<NOUT, 4>(a, s);
+  if (a.nin <= 8) return launch_bits_n<NOUT, 8>(a, s);
+  if constexpr (NOUT < 6) {  // wider outputs would spill: the host chunks them by 8 inputs
+    if (a.nin <= 12) return launch_bits_n<NOUT, 12>(a, s);
+    if (a.nin <= 16) return launch_bits_n<NOUT, 16>(a, s);
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace

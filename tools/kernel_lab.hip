@@ -1,0 +1,283 @@
+// Kernel lab: times encode-kernel variants against a no-math probe with the
+// same HBM access pattern, interleaved in one process (cdna_hip_programming.md
+// §5.4 rule 24). Dev tool, not part of the product.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/kernel_lab.hip -o build/kernel_lab
+#include "../lambdafs_amd/csrc/hrs_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace hrs;
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+namespace lab {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ void ld(const uint8_t* p, int lane, uint32_t (&w)[8]) {
+  const u32x4* a = reinterpret_cast<const u32x4*>(p + lane * 16);
+  const u32x4* b = reinterpret_cast<const u32x4*>(p + 1024 + lane * 16);
+  u32x4 x, y;
+  if (NT) {
+    x = __builtin_nontemporal_load(a);
+    y = __builtin_nontemporal_load(b);
+  } else {
+    x = *a;
+    y = *b;
+  }
+  w[0] = x[0]; w[1] = x[1]; w[2] = x[2]; w[3] = x[3];
+  w[4] = y[0]; w[5] = y[1]; w[6] = y[2]; w[7] = y[3];
+}
+
+template <bool NT>
+__device__ __forceinline__ void st(uint8_t* p, int lane, const uint32_t (&w)[8]) {
+  u32x4* a = reinterpret_cast<u32x4*>(p + lane * 16);
+  u32x4* b = reinterpret_cast<u32x4*>(p + 1024 + lane * 16);
+  u32x4 x = {w[0], w[1], w[2], w[3]}, y = {w[4], w[5], w[6], w[7]};
+  if (NT) {
+    __builtin_nontemporal_store(x, a);
+    __builtin_nontemporal_store(y, b);
+  } else {
+    *a = x;
+    *b = y;
+  }
+}
+
+// Same decomposition, no GF math: out_o = XOR of the rows (pattern ceiling).
+template <int K, int P, bool NT>
+__global__ void __launch_bounds__(kBlockThreads) probe_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      uint32_t w[8];
+      ld<NT>(a.in[r] + stripe * a.in_stride + off, lane, w);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] ^= w[q];
+    }
+#pragma unroll
+    for (int o = 0; o < P; ++o) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = acc[q] + o;
+      st<NT>(a.out[o] + stripe * a.out_stride + off, lane, v);
+    }
+  }
+}
+
+// The product's static encode body with load/store policy knobs.
+template <int K, int P, bool NT>
+__global__ void __launch_bounds__(kBlockThreads) encode_var_kernel(const RowArgs a) {
+  constexpr StaticPlan<K, P> plan{};
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    uint32_t acc[P][8];
+    uint32_t pend[P][8];
+    bool has[P][8];
+#pragma unroll
+    for (int o = 0; o < P; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc[o][q] = 0u;
+        pend[o][q] = 0u;
+        has[o][q] = false;
+      }
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      uint32_t w[8];
+      ld<NT>(a.in[r] + stripe * a.in_stride + off, lane, w);
+      bitslice(w);
+#pragma unroll
+      for (int o = 0; o < P; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if ((plan.mask[o][r][q] >> i) & 1) {
+              if (has[o][q]) {
+                acc[o][q] = xor3(acc[o][q], pend[o][q], w[i]);
+                has[o][q] = false;
+              } else {
+                pend[o][q] = w[i];
+                has[o][q] = true;
+              }
+            }
+    }
+#pragma unroll
+    for (int o = 0; o < P; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (has[o][q]) acc[o][q] ^= pend[o][q];
+#pragma unroll
+    for (int o = 0; o < P; ++o) {
+      bitslice(acc[o]);
+      st<NT>(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+  }
+}
+
+// The round-1 runtime kernel (one row of prefetch), kept for A/B.
+template <int NOUT>
+__global__ void __launch_bounds__(kBlockThreads) bitsliced_old_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t acc[NOUT][8];
+    if (a.accumulate) {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) {
+        load_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+        bitslice(acc[o]);
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+    }
+    uint32_t cur[8];
+    load_row(a.in[0] + in_base, lane, cur);
+    for (int r = 0; r < a.nin; ++r) {
+      uint32_t nxt[8];
+      if (r + 1 < a.nin) load_row(a.in[r + 1] + in_base, lane, nxt);
+      bitslice(cur);
+      uint32_t c[NOUT];
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) c[o] = a.coef[o][r];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) {
+          if ((c[o] >> b) & 1u) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[o][q] ^= cur[q];
+          }
+        }
+        if (b < 7) xtime(cur);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    }
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      bitslice(acc[o]);
+      store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+  }
+}
+
+}  // namespace lab
+
+int main(int argc, char** argv) {
+  const int S = argc > 1 ? atoi(argv[1]) : 1024;
+  const size_t L = 1 << 20;
+  const int k = 10, p = 4, n = 14;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 15;
+  uint8_t* buf;
+  CK(hipMalloc(&buf, (size_t)S * n * L));
+  CK(hipMemset(buf, 0x3c, (size_t)S * n * L));
+  uint8_t* copy_dst;
+  CK(hipMalloc(&copy_dst, (size_t)S * 7 * L));
+  RowArgs a{};
+  for (int c = 0; c < k; ++c) a.in[c] = buf + (size_t)(p + c) * L;
+  for (int r = 0; r < p; ++r) a.out[r] = buf + (size_t)r * L;
+  a.in_stride = a.out_stride = (uint64_t)n * L;
+  a.len = L;
+  a.nwin = L / kWindowBytes;
+  a.ntasks = a.nwin * S;
+  a.nin = k;
+  a.nout = p;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+
+  struct Var {
+    std::string name;
+    std::function<void()> run;
+    double bytes;
+    std::vector<float> ms;
+  };
+  auto occ = [&](const void* f) {
+    int b = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, kBlockThreads, 0));
+    return b;
+  };
+  const double enc_bytes = (double)(k + p) * L * S;
+  std::vector<Var> vars;
+  auto add_grid = [&](const char* nm, auto kern, unsigned grid) {
+    vars.push_back({std::string(nm) + " grid=" + std::to_string(grid),
+                    [=]() { hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlockThreads), 0, 0, a); }, enc_bytes, {}});
+  };
+  const unsigned all_tasks = (unsigned)((a.ntasks + kWavesPerBlock - 1) / kWavesPerBlock);
+  const char* which = argc > 3 ? argv[3] : "sweep";
+  if (std::string(which) == "sweep") {
+    for (unsigned g : {256u, 512u, 768u, 1024u, 2048u})
+      add_grid("product encode_static NT", encode_static_kernel<10, 4>, g);
+    for (unsigned g : {512u, 1024u}) add_grid("lab encode NT", lab::encode_var_kernel<10, 4, true>, g);
+    add_grid("probe10x4 NT", lab::probe_kernel<10, 4, true>, 512);
+  }
+  vars.push_back({"hipMemcpyAsync D2D 7/14 of batch", [=]() {
+                    (void)hipMemcpyAsync(copy_dst, buf, (size_t)S * 7 * L, hipMemcpyDeviceToDevice, 0);
+                  }, 2.0 * S * 7 * L, {}});
+  {
+    RowArgs d = a;  // decode 1 erasure through the runtime kernels
+    d.nout = 1;
+    for (int c = 0; c < k; ++c) d.coef[0][c] = (uint8_t)(17 * c + 3);
+    d.out[0] = copy_dst;
+    d.out_stride = L;
+    auto knew = bitsliced_kernel<1, 12>;
+    auto kold = lab::bitsliced_old_kernel<1>;
+    for (unsigned g : {512u, 768u, 1024u, 2048u}) {
+      vars.push_back({"product bitsliced<1,12> (decode) grid=" + std::to_string(g), [=]() {
+                        hipLaunchKernelGGL(knew, dim3(g), dim3(kBlockThreads), 0, 0, d);
+                      }, (double)(k + 1) * L * S, {}});
+      vars.push_back({"old bitsliced<1> (decode) grid=" + std::to_string(g), [=]() {
+                        hipLaunchKernelGGL(kold, dim3(g), dim3(kBlockThreads), 0, 0, d);
+                      }, (double)(k + 1) * L * S, {}});
+    }
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& v : vars) v.run();  // warm
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < rounds; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(e0, 0));
+      v.run();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms);
+    }
+  for (auto& v : vars) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const float med = v.ms[v.ms.size() / 2], mn = v.ms[0];
+    printf("%-48s median %8.3f ms  min %8.3f ms  %7.1f GB/s (median)\n", v.name.c_str(), med, mn,
+           v.bytes / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}
