@@ -189,6 +189,14 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_old_kernel(const RowA
   }
 }
 
+// Classic grid-stride float4 copy (the MI355X_MICROARCH.md copy-peak shape).
+template <bool NT>
+__global__ void __launch_bounds__(256) copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    else dst[i] = src[i];
+  }
+}
 }  // namespace lab
 
 int main(int argc, char** argv) {
@@ -197,10 +205,11 @@ int main(int argc, char** argv) {
   const int k = 10, p = 4, n = 14;
   const int rounds = argc > 2 ? atoi(argv[2]) : 15;
   uint8_t* buf;
-  CK(hipMalloc(&buf, (size_t)S * n * L));
-  CK(hipMemset(buf, 0x3c, (size_t)S * n * L));
+  const size_t buf_bytes = (size_t)S * n * (L + 65536 + 2048);
+  CK(hipMalloc(&buf, buf_bytes));
+  CK(hipMemset(buf, 0x3c, buf_bytes));
   uint8_t* copy_dst;
-  CK(hipMalloc(&copy_dst, (size_t)S * 7 * L));
+  CK(hipMalloc(&copy_dst, (size_t)S * 7 * L + (size_t)S * (65536 + 2048)));
   RowArgs a{};
   for (int c = 0; c < k; ++c) a.in[c] = buf + (size_t)(p + c) * L;
   for (int r = 0; r < p; ++r) a.out[r] = buf + (size_t)r * L;
@@ -256,6 +265,68 @@ int main(int argc, char** argv) {
       vars.push_back({"old bitsliced<1> (decode) grid=" + std::to_string(g), [=]() {
                         hipLaunchKernelGGL(kold, dim3(g), dim3(kBlockThreads), 0, 0, d);
                       }, (double)(k + 1) * L * S, {}});
+    }
+  }
+  if (std::string(which) == "sweep") {
+    // classic copy at several grids: 7/14 of the batch
+    const size_t nvec = (size_t)S * 7 * L / 16;
+    auto cnt = lab::copy_kernel<true>;
+    auto cpl = lab::copy_kernel<false>;
+    for (unsigned g : {1024u, 2048u, 4096u, 16384u}) {
+      vars.push_back({"classic copy NT grid=" + std::to_string(g), [=]() {
+                        hipLaunchKernelGGL(cnt, dim3(g), dim3(256), 0, 0, (const lab::u32x4*)buf, (lab::u32x4*)copy_dst, nvec);
+                      }, 2.0 * S * 7 * L, {}});
+      vars.push_back({"classic copy plain grid=" + std::to_string(g), [=]() {
+                        hipLaunchKernelGGL(cpl, dim3(g), dim3(256), 0, 0, (const lab::u32x4*)buf, (lab::u32x4*)copy_dst, nvec);
+                      }, 2.0 * S * 7 * L, {}});
+    }
+    // decode right after encode, reading parity location 3 the encode just wrote
+    RowArgs d = a;
+    d.nout = 1;
+    const int locs[10] = {3, 5, 6, 7, 8, 9, 10, 11, 12, 13};
+    for (int c = 0; c < k; ++c) {
+      d.in[c] = buf + (size_t)locs[c] * L;
+      d.coef[0][c] = (uint8_t)(17 * c + 3);
+    }
+    d.out[0] = copy_dst;
+    d.out_stride = L;
+    auto kenc = encode_static_kernel<10, 4>;
+    auto kdec = bitsliced_kernel<1, 12>;
+    for (unsigned g : {512u, 768u}) {
+      vars.push_back({"PAIR encode+decode(loc3) dec grid=" + std::to_string(g), [=]() {
+                        hipLaunchKernelGGL(kenc, dim3(512), dim3(kBlockThreads), 0, 0, a);
+                        hipLaunchKernelGGL(kdec, dim3(g), dim3(kBlockThreads), 0, 0, d);
+                      }, enc_bytes + (double)(k + 1) * L * S, {}});
+      vars.push_back({"decode(loc3) alone grid=" + std::to_string(g), [=]() {
+                        hipLaunchKernelGGL(kdec, dim3(g), dim3(kBlockThreads), 0, 0, d);
+                      }, (double)(k + 1) * L * S, {}});
+    }
+  }
+  if (std::string(which) == "pitch") {
+    // row pitch sweep: rows at buf + (stripe * n + r) * (L + pad); buffer sized for the max pad
+    auto kenc = encode_static_kernel<10, 4>;
+    auto kdec = bitsliced_kernel<1, 12>;
+    auto kread = lab::probe_kernel<10, 1, true>;
+    for (size_t pad : {(size_t)0, (size_t)256, (size_t)2048, (size_t)4096, (size_t)6144, (size_t)8192,
+                       (size_t)12288, (size_t)65536 + 2048}) {
+      const size_t P = L + pad;
+      if ((size_t)S * n * P > (size_t)S * n * L + (size_t)S * n * (65536 + 2048)) continue;
+      RowArgs e = a;
+      for (int c = 0; c < k; ++c) e.in[c] = buf + (size_t)(p + c) * P;
+      for (int r = 0; r < p; ++r) e.out[r] = buf + (size_t)r * P;
+      e.in_stride = e.out_stride = (uint64_t)n * P;
+      RowArgs d = e;
+      d.nout = 1;
+      for (int c = 0; c < k; ++c) d.coef[0][c] = (uint8_t)(17 * c + 3);
+      d.out[0] = copy_dst;
+      d.out_stride = P;
+      const std::string t = " pad=" + std::to_string(pad);
+      vars.push_back({"encode grid=512" + t, [=]() { hipLaunchKernelGGL(kenc, dim3(512), dim3(kBlockThreads), 0, 0, e); },
+                      enc_bytes, {}});
+      vars.push_back({"decode<1,12> grid=512" + t, [=]() { hipLaunchKernelGGL(kdec, dim3(512), dim3(kBlockThreads), 0, 0, d); },
+                      (double)(k + 1) * L * S, {}});
+      vars.push_back({"probe read10x1 grid=512" + t, [=]() { hipLaunchKernelGGL(kread, dim3(512), dim3(kBlockThreads), 0, 0, d); },
+                      (double)(k + 1) * L * S, {}});
     }
   }
   hipEvent_t e0, e1;
