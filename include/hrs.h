@@ -51,6 +51,13 @@ enum {
 
 typedef struct hrs_codec hrs_codec;
 
+/* Code families behind the same boundary (hops codec table,
+ * hadoop-hdfs/src/main/resources/erasure-coding-default.xml:13-56). */
+enum {
+  HRS_CODE_RS = 0,  /* "rs":  io.hops.erasure_coding.ReedSolomonCode (ReedSolomonCode.java) */
+  HRS_CODE_XOR = 1  /* "xor": io.hops.erasure_coding.XORCode (XORCode.java), parity_size == 1 */
+};
+
 #define HRS_DEVICE_NONE (-2)
 
 typedef struct hrs_opts {
@@ -66,6 +73,11 @@ typedef struct hrs_opts {
  * parity_size). Requires stripe_size >= 1, parity_size >= 1 and
  * stripe_size + parity_size < 256 (ReedSolomonCode.java:57). opts may be NULL. */
 hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out);
+/* Same for any code family: HRS_CODE_RS (== hrs_create) or HRS_CODE_XOR
+ * (XORCode.init asserts parity_size == 1, XORCode.java:46-51). */
+hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts,
+                           hrs_codec** out);
+int hrs_code_kind(const hrs_codec* codec);
 void hrs_destroy(hrs_codec* codec);
 /* Last error message of this handle ("" if none); handle may be NULL for create errors. */
 const char* hrs_last_error(const hrs_codec* codec);
@@ -85,7 +97,8 @@ int hrs_symbol_size(const hrs_codec* codec);
 hrs_status hrs_locations_to_read(const hrs_codec* codec, const int* erased, int num_erased,
                                  int* to_read);
 
-/* p x k encode matrix G (row-major): parity_r = XOR_c G[r][c] * data_c. */
+/* p x k encode matrix G (row-major): parity_r = XOR_c G[r][c] * data_c.
+ * XOR code: one row of ones (XORCode.encodeBulk, XORCode.java:99-113). */
 hrs_status hrs_encode_matrix(const hrs_codec* codec, uint8_t* g);
 
 /* num_erased x n decode matrix D (row-major, n = k + p, hops order):
@@ -109,6 +122,10 @@ hrs_status hrs_decode_matrix(const hrs_codec* codec, const int* erased, int num_
  * untouched; the Java/Python shims restore that side effect when asked. */
 hrs_status hrs_encode(hrs_codec* codec, const uint8_t* const* inputs, uint8_t* const* outputs,
                       size_t len);
+
+/* XOR code: decode needs exactly one erased location; the output is the XOR
+ * of every other row (XORCode.decodeBulk, XORCode.java:115-145; NULL rows
+ * count as the zeros the reference reads there). */
 
 /* ReedSolomonCode.decodeBulk(readBufs, writeBufs, erased, toRead, notToRead)
  * (ReedSolomonCode.java:191-211): read_bufs[n] in hops order (a row may be

@@ -22,9 +22,12 @@ HRS_EDEVICE = 3
 HRS_ENOMEM = 4
 HRS_EALIGN = 5
 
+HRS_CODE_RS = 0
+HRS_CODE_XOR = 1
+
 # Every entry point declared in include/hrs.h (checked by tests/test_abi.py).
 EXPORTS = (
-    "hrs_create", "hrs_destroy", "hrs_last_error", "hrs_version",
+    "hrs_create", "hrs_create_code", "hrs_code_kind", "hrs_destroy", "hrs_last_error", "hrs_version",
     "hrs_stripe_size", "hrs_parity_size", "hrs_symbol_size",
     "hrs_locations_to_read", "hrs_encode_matrix", "hrs_decode_matrix",
     "hrs_encode", "hrs_decode", "hrs_decode3",
@@ -62,6 +65,8 @@ def lib():
     U8P = ctypes.c_void_p
     sigs = {
         "hrs_create": ([I, I, ctypes.POINTER(HipOpts), ctypes.POINTER(P)], I),
+        "hrs_create_code": ([I, I, I, ctypes.POINTER(HipOpts), ctypes.POINTER(P)], I),
+        "hrs_code_kind": ([P], I),
         "hrs_destroy": ([P], None),
         "hrs_last_error": ([P], ctypes.c_char_p),
         "hrs_version": ([], ctypes.c_char_p),

@@ -25,6 +25,7 @@ using hrs::RowArgs;
 namespace gf = hrs::gf;
 
 struct hrs_codec {
+  int kind = HRS_CODE_RS;
   int k = 0;
   int p = 0;
   int n = 0;
@@ -180,6 +181,34 @@ const std::vector<uint8_t>* cached_decode_matrix(hrs_codec* c, const int* erased
 
 // ---------------------------------------------------------------- dispatch
 
+// The matrix a 5-arg decodeBulk applies (ne x n), per code family.
+//  RS : cached closed-form matrix; more than p not-to-read locations throw in
+//       the Java (errSignature is sized p, ReedSolomonCode.java:60).
+//  XOR: exactly one erased location; the output is the XOR of every other row
+//       (XORCode.java:115-145 ignores toRead/notToRead). Rows the caller passes
+//       as NULL are the zeros the reference reads there (StripeReader.java:111-120).
+hrs_status decode5_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
+                          const uint8_t* const* rows, std::vector<uint8_t>& tmp, const uint8_t** out) {
+  for (int t = 0; t < ne; ++t)
+    if (erased[t] < 0 || erased[t] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  if (c->kind == HRS_CODE_XOR) {
+    if (ne != 1) return fail(c, HRS_EINVAL, "XOR code decodes exactly one erased location (got %d)", ne);
+    tmp.assign(c->n, 1);
+    tmp[erased[0]] = 0;
+    if (rows)
+      for (int l = 0; l < c->n; ++l)
+        if (!rows[l]) tmp[l] = 0;
+    *out = tmp.data();
+    return HRS_OK;
+  }
+  if (nn > c->p) return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
+  hrs_status st;
+  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, ntr, nn, 1, &st);
+  if (!d) return st;
+  *out = d->data();
+  return HRS_OK;
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // out_o = XOR_i m[o][i] * in_i for every stripe. `static_kp` allows the
@@ -250,6 +279,42 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
   }
 
   const int nlive = static_cast<int>(live.size());
+  // A single output whose live coefficients are all 1 is a plain XOR of rows
+  // (the XOR code, XORCode.java:99-145): no bit-slicing needed.
+  bool all_ones = (nout == 1) && nwin > 0 && mode == 0;
+  for (int i : live) all_ones &= m[i] == 1;
+  if (all_ones) {
+    for (int i0 = 0; i0 < nlive; i0 += hrs::kMaxInRuntime) {
+      const int ni = std::min(hrs::kMaxInRuntime, nlive - i0);
+      RowArgs a{};
+      for (int i = 0; i < ni; ++i) a.in[i] = in_rows[live[i0 + i]];
+      a.out[0] = out_rows[0];
+      a.in_stride = in_stride;
+      a.out_stride = out_stride;
+      a.len = len;
+      a.nwin = nwin;
+      a.ntasks = nwin * nstripes;
+      a.nin = ni;
+      a.nout = 1;
+      a.accumulate = i0 > 0;
+      hipError_t e = hrs::launch_xor(a, s);
+      if (e != hipSuccess) return hip_fail(c, e, "xor launch");
+      if (tail > 0) {
+        RowArgs b = a;
+        for (int i = 0; i < ni; ++i) {
+          b.in[i] = a.in[i] + tail_off;
+          b.coef[0][i] = 1;
+        }
+        b.out[0] = a.out[0] + tail_off;
+        b.len = tail;
+        b.nwin = 0;
+        b.ntasks = tail * nstripes;
+        e = hrs::launch_bytewise(b, s);
+        if (e != hipSuccess) return hip_fail(c, e, "bytewise launch");
+      }
+    }
+    return HRS_OK;
+  }
   for (int o0 = 0; o0 < nout; o0 += hrs::kMaxOut) {
     const int no = std::min(hrs::kMaxOut, nout - o0);
     const int chunk = hrs::runtime_in_chunk(no);
@@ -341,6 +406,14 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   return HRS_OK;
 }
 
+void init_encode_matrix(hrs_codec* c) {
+  c->g.resize(static_cast<size_t>(c->p) * c->k);
+  if (c->kind == HRS_CODE_XOR)
+    std::fill(c->g.begin(), c->g.end(), 1);  // XORCode.encodeBulk, XORCode.java:99-113
+  else
+    gf::encode_matrix(c->k, c->p, c->g.data());
+}
+
 bool sorted_unique_ok(const int* v, int nv, int n) {
   for (int i = 0; i < nv; ++i)
     if (v[i] < 0 || v[i] >= n) return false;
@@ -354,8 +427,17 @@ extern "C" {
 const char* hrs_version(void) { return "hrs 0.1.0 (gfx950)"; }
 
 hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out) {
+  return hrs_create_code(HRS_CODE_RS, stripe_size, parity_size, opts, out);
+}
+
+int hrs_code_kind(const hrs_codec* c) { return c ? c->kind : -1; }
+
+hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out) {
   if (!out) return fail(nullptr, HRS_EINVAL, "out is NULL");
   *out = nullptr;
+  if (code != HRS_CODE_RS && code != HRS_CODE_XOR) return fail(nullptr, HRS_EINVAL, "unknown code family %d", code);
+  if (code == HRS_CODE_XOR && parity_size != 1)
+    return fail(nullptr, HRS_EINVAL, "XOR code needs parity size 1 (XORCode.java:47), got %d", parity_size);
   if (stripe_size < 1 || parity_size < 1 || stripe_size + parity_size >= gf::kFieldSize ||
       parity_size > gf::kMaxParity)
     return fail(nullptr, HRS_EINVAL, "unsupported RS(%d,%d): need k>=1, 1<=p<=%d, k+p<256", stripe_size,
@@ -370,8 +452,8 @@ hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hr
     c->p = parity_size;
     c->n = stripe_size + parity_size;
     c->device = HRS_DEVICE_NONE;
-    c->g.resize(static_cast<size_t>(parity_size) * stripe_size);
-    gf::encode_matrix(stripe_size, parity_size, c->g.data());
+    c->kind = code;
+    init_encode_matrix(c);
     *out = c;
     return HRS_OK;
   }
@@ -388,8 +470,8 @@ hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hr
   c->p = parity_size;
   c->n = stripe_size + parity_size;
   c->device = dev;
-  c->g.resize(static_cast<size_t>(parity_size) * stripe_size);
-  gf::encode_matrix(stripe_size, parity_size, c->g.data());
+  c->kind = code;
+  init_encode_matrix(c);
   {
     DeviceGuard g(dev);
     e = g.ok ? hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) : hipErrorInvalidDevice;
@@ -458,7 +540,13 @@ hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, con
   auto* c = const_cast<hrs_codec*>(cc);
   if (!c || !d || ne < 0 || nn < 0 || (ne && !erased) || (nn && !ntr)) return HRS_EINVAL;
   std::vector<uint8_t> m;
-  hrs_status st = build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, m);
+  hrs_status st;
+  if (c->kind == HRS_CODE_XOR) {
+    const uint8_t* x = nullptr;
+    st = decode5_matrix(c, erased, ne, ntr, nn, nullptr, m, &x);
+  } else {
+    st = build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, m);
+  }
   if (st == HRS_OK && !m.empty()) std::memcpy(d, m.data(), m.size());
   return st;
 }
@@ -466,7 +554,7 @@ hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, con
 hrs_status hrs_encode(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
   if (!c) return HRS_EINVAL;
   if (!inputs || !outputs) return fail(c, HRS_EINVAL, "inputs/outputs is NULL");
-  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, true);
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind == HRS_CODE_RS);
 }
 
 hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
@@ -477,19 +565,25 @@ hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* co
     return fail(c, HRS_EINVAL, "bad decode arguments");
   if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) || (to_read && !sorted_unique_ok(to_read, nr, c->n)))
     return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
-  // The Java sizes errSignature by p (ReedSolomonCode.java:60): more than p
-  // not-to-read locations throw there.
-  if (nn > c->p) return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
-  hrs_status st;
-  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, ntr, nn, 1, &st);
-  if (!d) return st;
-  return host_apply(c, d->data(), ne, c->n, read_bufs, write_bufs, len, false);
+  if (ne == 0 && c->kind == HRS_CODE_RS) return HRS_OK;
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d);
+  if (st != HRS_OK) return st;
+  return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
 }
 
 hrs_status hrs_decode3(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
                        int ne, size_t len) {
   if (!c) return HRS_EINVAL;
   if (ne < 0 || (ne > 0 && (!read_bufs || !write_bufs || !erased))) return fail(c, HRS_EINVAL, "bad decode3 arguments");
+  if (c->kind == HRS_CODE_XOR) {  // XORCode.decodeBulk 3-arg == 5-arg (XORCode.java:140-145)
+    std::vector<uint8_t> tmp;
+    const uint8_t* d = nullptr;
+    hrs_status st = decode5_matrix(c, erased, ne, nullptr, 0, read_bufs, tmp, &d);
+    if (st != HRS_OK) return st;
+    return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
+  }
   if (ne == 0) return HRS_OK;  // ReedSolomonCode.java:170-172
   if (ne > c->p) return fail(c, HRS_EINVAL, "%d erasures > parity size %d", ne, c->p);  // errSignature[p]
   hrs_status st;
@@ -505,7 +599,7 @@ hrs_status hrs_encode_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   return run_apply(c, c->g.data(), c->p, c->k, in_rows, in_stride, out_rows, out_stride, len, nstripes,
-                   static_cast<hipStream_t>(stream), true);
+                   static_cast<hipStream_t>(stream), c->kind == HRS_CODE_RS);
 }
 
 hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_stride, uint8_t* const* out_rows,
@@ -514,13 +608,14 @@ hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_st
   if (!c) return HRS_EINVAL;
   if (!rows || ne < 0 || nn < 0 || (ne > 0 && (!out_rows || !erased)) || (nn > 0 && !ntr))
     return fail(c, HRS_EINVAL, "bad decode arguments");
-  if (nn > c->p) return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
-  hrs_status st;
-  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, ntr, nn, 1, &st);
-  if (!d) return st;
+  if (ne == 0 && c->kind == HRS_CODE_RS) return HRS_OK;
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, rows, tmp, &d);
+  if (st != HRS_OK) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
-  return run_apply(c, d->data(), ne, c->n, rows, in_stride, out_rows, out_stride, len, nstripes,
+  return run_apply(c, d, ne, c->n, rows, in_stride, out_rows, out_stride, len, nstripes,
                    static_cast<hipStream_t>(stream), false);
 }
 

@@ -243,6 +243,44 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
   }
 }
 
+// ------------------------------------------------------------- XOR kernel
+
+// out[0] = XOR of the nin input rows (XOR code, XORCode.java:99-145; also any
+// single-output matrix of ones). No bit-slicing: three rows per v_bitop3.
+template <int NINB>
+__global__ void __launch_bounds__(kBlockThreads) xor_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const int nin = a.nin;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t rows[NINB][8];
+#pragma unroll
+    for (int r = 0; r < NINB; ++r)
+      if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
+    uint32_t acc[8];
+    if (a.accumulate) {
+      load_row(a.out[0] + stripe * a.out_stride + off, lane, acc);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < NINB; r += 2) {
+      if (r + 1 < nin) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = xor3(acc[q], rows[r][q], rows[r + 1][q]);
+      } else if (r < nin) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] ^= rows[r][q];
+      }
+    }
+    store_row(a.out[0] + stripe * a.out_stride + off, lane, acc);
+  }
+}
+
 // --------------------------------------------- byte-granular kernel (any alignment)
 
 // One byte column per lane, log/antilog tables in LDS. Serves rows that are
@@ -382,6 +420,21 @@ hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s) {
     case 8: return launch_bits<8>(a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+template <int NINB>
+hipError_t launch_xor_n(const RowArgs& a, hipStream_t s) {
+  auto kern = xor_kernel<NINB>;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_xor(const RowArgs& a, hipStream_t s) {
+  if (a.nin <= 4) return launch_xor_n<4>(a, s);
+  if (a.nin <= 8) return launch_xor_n<8>(a, s);
+  if (a.nin <= 12) return launch_xor_n<12>(a, s);
+  if (a.nin <= 16) return launch_xor_n<16>(a, s);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s) {

@@ -141,17 +141,13 @@ class _Rows:
 
 # ------------------------------------------------------------ the RS codec
 
-class HipReedSolomonCode(ErasureCode):
-    """Drop-in for ReedSolomonCode (ReedSolomonCode.java:27-308) on MI355X.
+class _HipErasureCode(ErasureCode):
+    """Common HIP-backed implementation: bulk paths, matrices, lifecycle."""
 
-    zero_inputs_after_encode: the reference encodeBulk zeroes its `inputs`
-    (the bulk remainder of GaloisField.java:326-338 runs in place);
-    True (default) restores that side effect for host rows.
-    """
+    CODE_KIND = _lib.HRS_CODE_RS
+    JAVA_CLASS = None
 
-    JAVA_CLASS = "io.hops.erasure_coding.HipReedSolomonCode"
-
-    def __init__(self, stripeSize=None, paritySize=None, device=None, zero_inputs_after_encode=True):
+    def __init__(self, stripeSize=None, paritySize=None, device=None, zero_inputs_after_encode=False):
         self._h = None
         self._k = self._p = 0
         self._device = device
@@ -170,7 +166,7 @@ class HipReedSolomonCode(ErasureCode):
         opts = _lib.HipOpts()
         opts.device = -1 if self._device is None else int(self._device)
         h = ctypes.c_void_p()
-        check(L.hrs_create(int(k), int(p), ctypes.byref(opts), ctypes.byref(h)))
+        check(L.hrs_create_code(self.CODE_KIND, int(k), int(p), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
         self._k, self._p = int(k), int(p)
 
@@ -256,12 +252,15 @@ class HipReedSolomonCode(ErasureCode):
         L = _lib.lib()
         three = locationsNotToRead is None
         if three:
-            if not erasedLocations:
+            if not erasedLocations and self.CODE_KIND == _lib.HRS_CODE_RS:
                 return
             reads = _Rows(readBufs, writable=False)
             writes = _Rows(writeBufs, writable=True)
             if reads.device is not None:
-                m = self.decodeMatrix(erasedLocations, erasedLocations, zero_not_to_read=False)
+                if self.CODE_KIND == _lib.HRS_CODE_XOR:
+                    m = self.decodeMatrix(erasedLocations, [])
+                else:
+                    m = self.decodeMatrix(erasedLocations, erasedLocations, zero_not_to_read=False)
                 self._apply_dev(m, reads, writes)
                 return
             self._check(L.hrs_decode3(self._handle(), reads.ptrs, writes.ptrs, int_array(erasedLocations),
@@ -273,7 +272,7 @@ class HipReedSolomonCode(ErasureCode):
         reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
                       writable=False, allow_none=True)
         writes = _Rows(writeBufs, writable=True)
-        if not erasedLocations:
+        if not erasedLocations and self.CODE_KIND == _lib.HRS_CODE_RS:
             return
         if reads.device is not None:
             stream = _lib.torch.cuda.current_stream(reads.device).cuda_stream
@@ -291,6 +290,20 @@ class HipReedSolomonCode(ErasureCode):
         m = np.ascontiguousarray(m, dtype=np.uint8)
         self._check(_lib.lib().hrs_apply_dev(self._handle(), m.ctypes.data, m.shape[0], m.shape[1], reads.ptrs, 0,
                                              writes.ptrs, 0, reads.len, 1, stream))
+
+class HipReedSolomonCode(_HipErasureCode):
+    """Drop-in for ReedSolomonCode (ReedSolomonCode.java:27-308) on MI355X.
+
+    zero_inputs_after_encode: the reference encodeBulk zeroes its `inputs`
+    (the bulk remainder of GaloisField.java:326-338 runs in place);
+    True (default) restores that side effect for host rows.
+    """
+
+    CODE_KIND = _lib.HRS_CODE_RS
+    JAVA_CLASS = "io.hops.erasure_coding.HipReedSolomonCode"
+
+    def __init__(self, stripeSize=None, paritySize=None, device=None, zero_inputs_after_encode=True):
+        super().__init__(stripeSize, paritySize, device, zero_inputs_after_encode)
 
     # -- scalar (one symbol column; still computed by the GPU engine)
     def encode(self, message, parity):
@@ -331,6 +344,35 @@ class HipReedSolomonCode(ErasureCode):
         self.decodeBulk(rows, outs, list(erasedLocations), toread, ntr)
         for i in range(len(erasedLocations)):
             erasedValues[i] = int(outs[i][0])
+
+
+
+class HipXORCode(_HipErasureCode):
+    """Drop-in for XORCode (hops-erasure-coding/.../XORCode.java:24-146):
+    one parity row = XOR of the data rows; repair of one location = XOR of
+    all other rows. Inputs are left untouched, as in the Java."""
+
+    CODE_KIND = _lib.HRS_CODE_XOR
+    JAVA_CLASS = "io.hops.erasure_coding.HipXORCode"
+
+    def encode(self, message, parity):
+        """XORCode.encode (XORCode.java:54-61)."""
+        if len(message) != self._k or len(parity) != 1:
+            raise ValueError("message/parity length mismatch")
+        ins = [np.array([_symbol(v)], dtype=np.uint8) for v in message]
+        out = [np.zeros(1, dtype=np.uint8)]
+        self.encodeBulk(ins, out)
+        parity[0] = int(out[0][0])
+
+    def decode(self, data, erasedLocations, erasedValues, locationsToRead=None, locationsNotToRead=None):
+        """XORCode.decode (XORCode.java:63-83): a no-op unless exactly one
+        location is erased; data is not modified."""
+        if len(erasedLocations) != 1:
+            return
+        rows = [np.array([_symbol(v)], dtype=np.uint8) for v in data]
+        out = [np.zeros(1, dtype=np.uint8)]
+        self.decodeBulk(rows, out, list(erasedLocations))
+        erasedValues[0] = int(out[0][0])
 
 
 def _symbol(v):

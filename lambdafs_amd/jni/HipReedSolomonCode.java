@@ -16,10 +16,6 @@ import java.io.IOException;
 import java.util.Arrays;
 
 public class HipReedSolomonCode extends ErasureCode {
-  static {
-    System.loadLibrary("hrs_jni");  // libhrs_jni.so -> libhrs.so
-  }
-
   private long nativeCodec;  // hrs_codec*, owned (cf. jni_common.c:35-70 "nativeCoder")
   private int stripeSize;
   private int paritySize;
@@ -41,7 +37,7 @@ public class HipReedSolomonCode extends ErasureCode {
     release();
     this.stripeSize = stripeSize;
     this.paritySize = paritySize;
-    this.nativeCodec = nativeCreate(stripeSize, paritySize);  // throws IllegalArgumentException / RuntimeException
+    this.nativeCodec = HrsNative.create(HrsNative.CODE_RS, stripeSize, paritySize);  // throws IllegalArgumentException / RuntimeException
   }
 
   /** Same result as ReedSolomonCode.encodeBulk (ReedSolomonCode.java:103-125). */
@@ -49,7 +45,7 @@ public class HipReedSolomonCode extends ErasureCode {
   public void encodeBulk(byte[][] inputs, byte[][] outputs) throws IOException {
     assert (stripeSize == inputs.length);
     assert (paritySize == outputs.length);
-    nativeEncode(nativeCodec, inputs, outputs, outputs[0].length);
+    HrsNative.encode(nativeCodec, inputs, outputs, outputs[0].length);
     // The Java bulk remainder zeroes its inputs (GaloisField.java:326-338); keep that contract.
     for (byte[] in : inputs) {
       Arrays.fill(in, (byte) 0);
@@ -63,7 +59,7 @@ public class HipReedSolomonCode extends ErasureCode {
     if (erasedLocations.length == 0) {
       return;
     }
-    nativeDecode(nativeCodec, readBufs, writeBufs, erasedLocations, locationsToRead,
+    HrsNative.decode(nativeCodec, readBufs, writeBufs, erasedLocations, locationsToRead,
         locationsNotToRead, readBufs[0].length);
   }
 
@@ -73,7 +69,7 @@ public class HipReedSolomonCode extends ErasureCode {
     if (erasedLocation.length == 0) {
       return;
     }
-    nativeDecode3(nativeCodec, readBufs, writeBufs, erasedLocation, readBufs[0].length);
+    HrsNative.decode3(nativeCodec, readBufs, writeBufs, erasedLocation, readBufs[0].length);
   }
 
   @Override
@@ -84,7 +80,7 @@ public class HipReedSolomonCode extends ErasureCode {
       in[i][0] = (byte) message[i];
     }
     try {
-      nativeEncode(nativeCodec, in, out, 1);
+      HrsNative.encode(nativeCodec, in, out, 1);
     } catch (IOException e) {
       throw new RuntimeException(e);
     }
@@ -113,7 +109,7 @@ public class HipReedSolomonCode extends ErasureCode {
     }
     byte[][] out = new byte[erasedLocations.length][1];
     try {
-      nativeDecode(nativeCodec, rows, out, erasedLocations, locationsToRead, locationsNotToRead, 1);
+      HrsNative.decode(nativeCodec, rows, out, erasedLocations, locationsToRead, locationsNotToRead, 1);
     } catch (IOException e) {
       throw new RuntimeException(e);
     }
@@ -139,7 +135,7 @@ public class HipReedSolomonCode extends ErasureCode {
 
   public synchronized void release() {
     if (nativeCodec != 0) {
-      nativeDestroy(nativeCodec);
+      HrsNative.destroy(nativeCodec);
       nativeCodec = 0;
     }
   }
@@ -149,17 +145,4 @@ public class HipReedSolomonCode extends ErasureCode {
     release();
     super.finalize();
   }
-
-  private static native long nativeCreate(int stripeSize, int paritySize);
-
-  private static native void nativeDestroy(long codec);
-
-  private static native void nativeEncode(long codec, byte[][] inputs, byte[][] outputs, int len)
-      throws IOException;
-
-  private static native void nativeDecode(long codec, byte[][] readBufs, byte[][] writeBufs,
-      int[] erased, int[] toRead, int[] notToRead, int len) throws IOException;
-
-  private static native void nativeDecode3(long codec, byte[][] readBufs, byte[][] writeBufs,
-      int[] erased, int len) throws IOException;
 }

@@ -1,0 +1,32 @@
+/*
+ * JNI entry points of libhrs_jni.so (hrs_jni.c), shared by the engine's codec
+ * classes. Mirrors the C ABI in include/hrs.h; the handle is an hrs_codec*.
+ * Not compiled in this repository's CI (no JDK): see INTEGRATION.md.
+ */
+package io.hops.erasure_coding;
+
+import java.io.IOException;
+
+final class HrsNative {
+  static final int CODE_RS = 0;   // HRS_CODE_RS
+  static final int CODE_XOR = 1;  // HRS_CODE_XOR
+
+  static {
+    System.loadLibrary("hrs_jni");  // libhrs_jni.so -> libhrs.so
+  }
+
+  private HrsNative() {
+  }
+
+  static native long create(int code, int stripeSize, int paritySize);
+
+  static native void destroy(long codec);
+
+  static native void encode(long codec, byte[][] inputs, byte[][] outputs, int len) throws IOException;
+
+  static native void decode(long codec, byte[][] readBufs, byte[][] writeBufs, int[] erased, int[] toRead,
+      int[] notToRead, int len) throws IOException;
+
+  static native void decode3(long codec, byte[][] readBufs, byte[][] writeBufs, int[] erased, int len)
+      throws IOException;
+}

@@ -1,5 +1,6 @@
 /*
- * JNI shim: io.hops.erasure_coding.HipReedSolomonCode -> libhrs.so (include/hrs.h).
+ * JNI shim: io.hops.erasure_coding.HrsNative (used by HipReedSolomonCode and
+ * HipXORCode) -> libhrs.so (include/hrs.h).
  *
  * Pattern of the existing native codec precedent, libhadoop's ISA-L shim
  * (hadoop-common/src/main/native/src/org/apache/hadoop/io/erasurecode/
@@ -30,8 +31,10 @@ static void throw_status(JNIEnv* env, hrs_status st, const hrs_codec* c) {
   if (k) (*env)->ThrowNew(env, k, hrs_last_error(c));
 }
 
-/* Pins every row of a byte[][]; NULL rows stay NULL. Returns the row count or -1. */
-static int pin_rows(JNIEnv* env, jobjectArray arr, jbyteArray* objs, uint8_t** ptrs) {
+/* Fetches the row objects of a byte[][] (no JNI call may run while rows are
+ * held critical, so every array is fetched before any row is pinned).
+ * Returns the row count or -1. */
+static int fetch_rows(JNIEnv* env, jobjectArray arr, jbyteArray* objs, uint8_t** ptrs) {
   if (!arr) return 0;
   jsize n = (*env)->GetArrayLength(env, arr);
   if (n > MAX_ROWS) return -1;
@@ -39,9 +42,13 @@ static int pin_rows(JNIEnv* env, jobjectArray arr, jbyteArray* objs, uint8_t** p
     objs[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, arr, i);
     ptrs[i] = NULL;
   }
-  for (jsize i = 0; i < n; i++)
-    if (objs[i]) ptrs[i] = (uint8_t*)(*env)->GetPrimitiveArrayCritical(env, objs[i], NULL);
   return (int)n;
+}
+
+/* Pins fetched rows with GetPrimitiveArrayCritical (zero-copy); NULL rows stay NULL. */
+static void pin_rows(JNIEnv* env, int n, jbyteArray* objs, uint8_t** ptrs) {
+  for (int i = 0; i < n; i++)
+    if (objs[i]) ptrs[i] = (uint8_t*)(*env)->GetPrimitiveArrayCritical(env, objs[i], NULL);
 }
 
 static void unpin_rows(JNIEnv* env, int n, jbyteArray* objs, uint8_t** ptrs, jint mode) {
@@ -49,11 +56,11 @@ static void unpin_rows(JNIEnv* env, int n, jbyteArray* objs, uint8_t** ptrs, jin
     if (objs[i] && ptrs[i]) (*env)->ReleasePrimitiveArrayCritical(env, objs[i], ptrs[i], mode);
 }
 
-JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeCreate(JNIEnv* env, jclass cls,
-                                                                                     jint k, jint p) {
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv* env, jclass cls, jint code, jint k,
+                                                                       jint p) {
   (void)cls;
   hrs_codec* c = NULL;
-  hrs_status st = hrs_create(k, p, NULL, &c);
+  hrs_status st = hrs_create_code(code, k, p, NULL, &c);
   if (st != HRS_OK) {
     throw_status(env, st, NULL);
     return 0;
@@ -61,22 +68,26 @@ JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeCr
   return (jlong)(intptr_t)c;
 }
 
-JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeDestroy(JNIEnv* env, jclass cls,
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_destroy(JNIEnv* env, jclass cls,
                                                                                      jlong h) {
   (void)env;
   (void)cls;
   hrs_destroy((hrs_codec*)(intptr_t)h);
 }
 
-JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeEncode(JNIEnv* env, jclass cls, jlong h,
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_encode(JNIEnv* env, jclass cls, jlong h,
                                                                                     jobjectArray inputs,
                                                                                     jobjectArray outputs, jint len) {
   (void)cls;
   hrs_codec* c = (hrs_codec*)(intptr_t)h;
   jbyteArray io[MAX_ROWS], oo[MAX_ROWS];
   uint8_t *ip[MAX_ROWS], *op[MAX_ROWS];
-  int ni = pin_rows(env, inputs, io, ip);
-  int no = pin_rows(env, outputs, oo, op);
+  int ni = fetch_rows(env, inputs, io, ip);
+  int no = fetch_rows(env, outputs, oo, op);
+  if (ni >= 0 && no >= 0) {
+    pin_rows(env, ni, io, ip);
+    pin_rows(env, no, oo, op);
+  }
   hrs_status st = (ni < 0 || no < 0) ? HRS_EINVAL : hrs_encode(c, (const uint8_t* const*)ip, op, (size_t)len);
   unpin_rows(env, no > 0 ? no : 0, oo, op, 0);
   unpin_rows(env, ni > 0 ? ni : 0, io, ip, JNI_ABORT);
@@ -91,7 +102,7 @@ static int copy_ints(JNIEnv* env, jintArray a, int* out) {
   return (int)n;
 }
 
-JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeDecode(
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_decode(
     JNIEnv* env, jclass cls, jlong h, jobjectArray readBufs, jobjectArray writeBufs, jintArray erased,
     jintArray toRead, jintArray notToRead, jint len) {
   (void)cls;
@@ -100,8 +111,12 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeDec
   int ne = copy_ints(env, erased, e), nr = copy_ints(env, toRead, r), nn = copy_ints(env, notToRead, ntr);
   jbyteArray io[MAX_ROWS], oo[MAX_ROWS];
   uint8_t *ip[MAX_ROWS], *op[MAX_ROWS];
-  int ni = pin_rows(env, readBufs, io, ip);
-  int no = pin_rows(env, writeBufs, oo, op);
+  int ni = fetch_rows(env, readBufs, io, ip);
+  int no = fetch_rows(env, writeBufs, oo, op);
+  if (ni >= 0 && no >= 0) {
+    pin_rows(env, ni, io, ip);
+    pin_rows(env, no, oo, op);
+  }
   hrs_status st = (ni < 0 || no < 0)
                       ? HRS_EINVAL
                       : hrs_decode(c, (const uint8_t* const*)ip, op, e, ne, r, nr, ntr, nn, (size_t)len);
@@ -110,7 +125,7 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeDec
   if (st != HRS_OK) throw_status(env, st, c);
 }
 
-JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeDecode3(
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_decode3(
     JNIEnv* env, jclass cls, jlong h, jobjectArray readBufs, jobjectArray writeBufs, jintArray erased, jint len) {
   (void)cls;
   hrs_codec* c = (hrs_codec*)(intptr_t)h;
@@ -118,8 +133,12 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HipReedSolomonCode_nativeDec
   int ne = copy_ints(env, erased, e);
   jbyteArray io[MAX_ROWS], oo[MAX_ROWS];
   uint8_t *ip[MAX_ROWS], *op[MAX_ROWS];
-  int ni = pin_rows(env, readBufs, io, ip);
-  int no = pin_rows(env, writeBufs, oo, op);
+  int ni = fetch_rows(env, readBufs, io, ip);
+  int no = fetch_rows(env, writeBufs, oo, op);
+  if (ni >= 0 && no >= 0) {
+    pin_rows(env, ni, io, ip);
+    pin_rows(env, no, oo, op);
+  }
   hrs_status st = (ni < 0 || no < 0) ? HRS_EINVAL : hrs_decode3(c, (const uint8_t* const*)ip, op, e, ne, (size_t)len);
   unpin_rows(env, no > 0 ? no : 0, oo, op, 0);
   unpin_rows(env, ni > 0 ? ni : 0, io, ip, JNI_ABORT);

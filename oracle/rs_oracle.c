@@ -372,3 +372,40 @@ int orc_rs_compute_error_locations(int k, int p, int* data, int* locations, int*
   free(syndrome);
   return ok;
 }
+
+/* ------------------------------------------------------------- XOR code */
+
+/* XORCode.encode, XORCode.java:54-61 */
+void orc_xor_encode(int k, const int* message, int* parity) {
+  parity[0] = message[0];
+  for (int i = 1; i < k; i++) parity[0] ^= message[i];
+}
+
+/* XORCode.decode 3-arg, XORCode.java:63-77: no-op unless exactly one erasure */
+void orc_xor_decode(int k, const int* data, const int* erased, int ne, int* values) {
+  if (ne != 1) return;
+  int skipIndex = erased[0];
+  int val = 0;
+  for (int i = 0; i < k + 1; i++) {
+    if (i == skipIndex) continue;
+    val ^= data[i];
+  }
+  values[0] = val;
+}
+
+/* XORCode.encodeBulk, XORCode.java:99-113 */
+void orc_xor_encode_bulk(int k, uint8_t* const* inputs, uint8_t* output, size_t len) {
+  for (size_t j = 0; j < len; j++) output[j] = inputs[0][j];
+  for (int i = 1; i < k; i++)
+    for (size_t j = 0; j < len; j++) output[j] ^= inputs[i][j];
+}
+
+/* XORCode.decodeBulk 3-arg, XORCode.java:115-138 (readBufs has k + 1 rows) */
+void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int erased, size_t len) {
+  for (size_t j = 0; j < len; j++) output[j] = 0;
+  for (int i = 0; i < k + 1; i++) {
+    if (i == erased) continue;
+    const uint8_t* input = read_bufs[i];
+    for (size_t j = 0; j < len; j++) output[j] ^= input[j];
+  }
+}

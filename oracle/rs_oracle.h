@@ -66,4 +66,11 @@ int orc_locations_to_read(int k, int p, const int* erased, int ne, int* out);
  * writes up to n locations (ascending) and their count. */
 int orc_rs_compute_error_locations(int k, int p, int* data, int* locations, int* nloc);
 
+/* XORCode (hops-erasure-coding/.../XORCode.java): encode :54-61, decode :63-83,
+ * encodeBulk :99-113, decodeBulk 3-arg :115-138 (5-arg delegates, :140-145). */
+void orc_xor_encode(int k, const int* message, int* parity);
+void orc_xor_decode(int k, const int* data, const int* erased, int ne, int* values);
+void orc_xor_encode_bulk(int k, uint8_t* const* inputs, uint8_t* output, size_t len);
+void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int erased, size_t len);
+
 #endif

@@ -59,6 +59,10 @@ def lib():
             "orc_rs_decode_bulk3": ([I, I, PP, PP, IP, I, S], None),
             "orc_locations_to_read": ([I, I, IP, I, IP], I),
             "orc_rs_compute_error_locations": ([I, I, IP, IP, IP], I),
+            "orc_xor_encode": ([I, IP, IP], None),
+            "orc_xor_decode": ([I, IP, IP, I, IP], None),
+            "orc_xor_encode_bulk": ([I, PP, ctypes.c_void_p, S], None),
+            "orc_xor_decode_bulk": ([I, PP, ctypes.c_void_p, I, S], None),
         }
         for name, (args, res) in sigs.items():
             f = getattr(_lib, name)
@@ -205,6 +209,34 @@ def compute_error_locations(k, p, data):
     nloc = ctypes.c_int(0)
     ok = lib().orc_rs_compute_error_locations(k, p, d, locs, ctypes.byref(nloc))
     return bool(ok), set(list(locs)[: nloc.value]), list(d)[: len(data)]
+
+
+# ------------------------------------------------------------------ XORCode
+
+def xor_encode(k, message):
+    par = _ints([0])
+    lib().orc_xor_encode(k, _ints(message), par)
+    return [par[0]]
+
+
+def xor_decode(k, data, erased):
+    vals = _ints([-1] * max(1, len(erased)))
+    lib().orc_xor_decode(k, _ints(data), _ints(erased), len(erased), vals)
+    return list(vals)[: len(erased)]
+
+
+def xor_encode_bulk(k, inputs):
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    out = np.zeros(rows[0].size, dtype=np.uint8)
+    lib().orc_xor_encode_bulk(k, _rowptrs(rows), out.ctypes.data, out.size)
+    return out
+
+
+def xor_decode_bulk(k, read_bufs, erased):
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in read_bufs]
+    out = np.zeros(rows[0].size, dtype=np.uint8)
+    lib().orc_xor_decode_bulk(k, _rowptrs(rows), out.ctypes.data, int(erased), out.size)
+    return out
 
 
 # Raw entry points for the CPU baseline (pointer arrays prepared once).
