@@ -197,6 +197,83 @@ __global__ void __launch_bounds__(256) copy_kernel(const u32x4* __restrict__ src
     else dst[i] = src[i];
   }
 }
+typedef __attribute__((address_space(3))) void lds_void;
+
+// Probe with rows staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction), then read back with ds_read_b128: is the DMA read path faster?
+template <int K, int P>
+__global__ void __launch_bounds__(kBlockThreads) probe_glds_kernel(const RowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  uint8_t* mine = smem + (threadIdx.x >> 6) * K * kWindowBytes;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const uint8_t* g = a.in[r] + stripe * a.in_stride + off + lane * 16;
+      __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(mine + r * kWindowBytes), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(g + 1024), (lds_void*)(mine + r * kWindowBytes + 1024), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x3F70);  // vmcnt(0): this wave's DMA has landed
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const uint4 x = *reinterpret_cast<const uint4*>(mine + r * kWindowBytes + lane * 16);
+      const uint4 y = *reinterpret_cast<const uint4*>(mine + r * kWindowBytes + 1024 + lane * 16);
+      acc[0] ^= x.x; acc[1] ^= x.y; acc[2] ^= x.z; acc[3] ^= x.w;
+      acc[4] ^= y.x; acc[5] ^= y.y; acc[6] ^= y.z; acc[7] ^= y.w;
+    }
+#pragma unroll
+    for (int o = 0; o < P; ++o) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = acc[q] + o;
+      st<true>(a.out[o] + stripe * a.out_stride + off, lane, v);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) before the slot is refilled
+  }
+}
+
+// Register-load probe that prefetches the next task's rows while finishing the current one.
+template <int K, int P>
+__global__ void __launch_bounds__(kBlockThreads) probe_prefetch_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  uint64_t t = wave_id_in_grid();
+  if (t >= a.ntasks) return;
+  uint32_t cur[K][8];
+  {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+#pragma unroll
+    for (int r = 0; r < K; ++r) ld<true>(a.in[r] + stripe * a.in_stride + off, lane, cur[r]);
+  }
+  for (; t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] ^= cur[r][q];
+    const uint64_t tn = t + nwaves;
+    if (tn < a.ntasks) {
+      const uint64_t sn = tn / a.nwin;
+      const uint64_t on = (tn - sn * a.nwin) * kWindowBytes;
+#pragma unroll
+      for (int r = 0; r < K; ++r) ld<true>(a.in[r] + sn * a.in_stride + on, lane, cur[r]);
+    }
+#pragma unroll
+    for (int o = 0; o < P; ++o) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = acc[q] + o;
+      st<true>(a.out[o] + stripe * a.out_stride + off, lane, v);
+    }
+  }
+}
 }  // namespace lab
 
 int main(int argc, char** argv) {
@@ -328,6 +405,30 @@ int main(int argc, char** argv) {
       vars.push_back({"probe read10x1 grid=512" + t, [=]() { hipLaunchKernelGGL(kread, dim3(512), dim3(kBlockThreads), 0, 0, d); },
                       (double)(k + 1) * L * S, {}});
     }
+  }
+  if (std::string(which) == "glds") {
+    auto pg = lab::probe_glds_kernel<10, 4>;
+    auto pg1 = lab::probe_glds_kernel<10, 1>;
+    auto pr = lab::probe_kernel<10, 4, true>;
+    auto pr1 = lab::probe_kernel<10, 1, true>;
+    auto pp = lab::probe_prefetch_kernel<10, 4>;
+    const size_t shm = (size_t)kWavesPerBlock * 10 * kWindowBytes;  // 80 KiB per block
+    CK(hipFuncSetAttribute((const void*)pg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    CK(hipFuncSetAttribute((const void*)pg1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    RowArgs d = a;
+    d.out[0] = copy_dst;
+    d.out_stride = L;
+    for (unsigned g : {256u, 512u}) {
+      const std::string t = " grid=" + std::to_string(g);
+      vars.push_back({"glds probe 10x4" + t, [=]() { hipLaunchKernelGGL(pg, dim3(g), dim3(kBlockThreads), shm, 0, a); }, enc_bytes, {}});
+      vars.push_back({"reg probe 10x4" + t, [=]() { hipLaunchKernelGGL(pr, dim3(g), dim3(kBlockThreads), 0, 0, a); }, enc_bytes, {}});
+      vars.push_back({"reg prefetch probe 10x4" + t, [=]() { hipLaunchKernelGGL(pp, dim3(g), dim3(kBlockThreads), 0, 0, a); }, enc_bytes, {}});
+      vars.push_back({"glds probe 10x1" + t, [=]() { hipLaunchKernelGGL(pg1, dim3(g), dim3(kBlockThreads), shm, 0, d); }, (double)(k + 1) * L * S, {}});
+      vars.push_back({"reg probe 10x1" + t, [=]() { hipLaunchKernelGGL(pr1, dim3(g), dim3(kBlockThreads), 0, 0, d); }, (double)(k + 1) * L * S, {}});
+    }
+    auto pe = encode_static_kernel<10, 4>;
+    vars.push_back({"product encode grid=512", [=]() {
+                      hipLaunchKernelGGL(pe, dim3(512), dim3(kBlockThreads), 0, 0, a); }, enc_bytes, {}});
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
