@@ -11,7 +11,9 @@ ORACLE   := oracle/liboracle.so
 SRCS     := lambdafs_amd/csrc/hrs_api.cpp lambdafs_amd/csrc/hrs_kernels.hip
 HDRS     := include/hrs.h lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp
 
-all: $(LIB) $(ORACLE)
+HARNESS  := tests/cpp/codec_harness
+
+all: $(LIB) $(ORACLE) $(HARNESS)
 
 build/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS)
 	@mkdir -p build
@@ -27,7 +29,12 @@ $(LIB): build/hrs_api.o build/hrs_kernels.o
 $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/rs_oracle.c
 
+# Test-only native harness (tests/cpp): the codec driven like Encoder/Decoder.
+$(HARNESS): tests/cpp/codec_harness.cpp include/hrs.hpp include/hrs.h $(LIB) $(ORACLE)
+	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs -Loracle -loracle -lz \
+	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
 clean:
-	rm -rf build $(LIB) $(ORACLE)
+	rm -rf build $(LIB) $(ORACLE) $(HARNESS)
 
 .PHONY: all clean

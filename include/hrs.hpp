@@ -1,0 +1,142 @@
+// hrs.hpp — header-only C++17 mirror of the hops codec plugin interface over
+// the C ABI in hrs.h, for native callers (the C++ analogue of the JNI shim).
+//
+//   hrs::ErasureCode        io.hops.erasure_coding.ErasureCode
+//                           (hadoop-hdfs/.../io/hops/erasure_coding/ErasureCode.java:25-182)
+//   hrs::HipReedSolomonCode ReedSolomonCode (hops-erasure-coding/.../ReedSolomonCode.java)
+//   hrs::HipXORCode         XORCode        (hops-erasure-coding/.../XORCode.java)
+//   hrs::IOException / hrs::TooManyErasedLocations  the Java exceptions
+//
+// Java's byte[][] rows carry their length; here rows are raw pointers plus one
+// `len` for the call, as Encoder.java:442 / Decoder.java:352 pass equal-length rows.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hrs.h"
+
+namespace hrs {
+
+class IOException : public std::runtime_error {
+ public:
+  explicit IOException(const std::string& m, int status = HRS_EDEVICE) : std::runtime_error(m), status_(status) {}
+  int status() const { return status_; }
+
+ private:
+  int status_;
+};
+
+// TooManyErasedLocations extends IOException (TooManyErasedLocations.java:26-31).
+class TooManyErasedLocations : public IOException {
+ public:
+  explicit TooManyErasedLocations(const std::string& m) : IOException(m, HRS_ETOOMANY) {}
+};
+
+inline void check(hrs_status st, const hrs_codec* c) {
+  if (st == HRS_OK) return;
+  const std::string msg = hrs_last_error(c);
+  if (st == HRS_ETOOMANY) throw TooManyErasedLocations(msg);
+  if (st == HRS_EINVAL) throw std::invalid_argument(msg);
+  throw IOException(msg, st);
+}
+
+class ErasureCode {
+ public:
+  virtual ~ErasureCode() = default;
+  virtual int stripeSize() const = 0;
+  virtual int paritySize() const = 0;
+  virtual int symbolSize() const = 0;
+  // ErasureCode.java:136-156 / :162-181
+  virtual void encodeBulk(const std::vector<uint8_t*>& inputs, const std::vector<uint8_t*>& outputs,
+                          size_t len) = 0;
+  virtual void decodeBulk(const std::vector<uint8_t*>& readBufs, const std::vector<uint8_t*>& writeBufs,
+                          size_t len, const std::vector<int>& erasedLocations,
+                          const std::vector<int>& locationsToRead,
+                          const std::vector<int>& locationsNotToRead) = 0;
+  // ErasureCode.java:89-113 — the k highest-index locations not erased, highest first.
+  std::vector<int> locationsToReadForDecode(const std::vector<int>& erasedLocations) const {
+    std::vector<int> out;
+    const int limit = stripeSize() + paritySize();
+    for (int loc = limit - 1; loc >= 0; --loc) {
+      bool erased = false;
+      for (int e : erasedLocations) erased |= e == loc;
+      if (!erased) {
+        out.push_back(loc);
+        if (static_cast<int>(out.size()) == stripeSize()) break;
+      }
+    }
+    if (static_cast<int>(out.size()) != stripeSize()) {
+      std::string s = "Locations ";
+      for (int e : erasedLocations) s += " " + std::to_string(e);
+      throw TooManyErasedLocations(s);
+    }
+    return out;
+  }
+};
+
+// Common owner of an hrs_codec handle.
+class HipCode : public ErasureCode {
+ public:
+  HipCode(int code, int k, int p, int device = -1) {
+    hrs_opts o{};
+    o.device = device;
+    hrs_codec* c = nullptr;
+    hrs_status st = hrs_create_code(code, k, p, &o, &c);
+    if (st != HRS_OK) check(st, nullptr);
+    h_ = c;
+  }
+  ~HipCode() override { hrs_destroy(h_); }
+  HipCode(const HipCode&) = delete;
+  HipCode& operator=(const HipCode&) = delete;
+
+  int stripeSize() const override { return hrs_stripe_size(h_); }
+  int paritySize() const override { return hrs_parity_size(h_); }
+  int symbolSize() const override { return hrs_symbol_size(h_); }
+  hrs_codec* handle() const { return h_; }
+
+  void encodeBulk(const std::vector<uint8_t*>& inputs, const std::vector<uint8_t*>& outputs, size_t len) override {
+    if (static_cast<int>(inputs.size()) != stripeSize() || static_cast<int>(outputs.size()) != paritySize())
+      throw std::invalid_argument("encodeBulk: row counts do not match the codec");
+    std::vector<const uint8_t*> in(inputs.begin(), inputs.end());
+    check(hrs_encode(h_, in.data(), outputs.data(), len), h_);
+  }
+
+  void decodeBulk(const std::vector<uint8_t*>& readBufs, const std::vector<uint8_t*>& writeBufs, size_t len,
+                  const std::vector<int>& erased, const std::vector<int>& toRead,
+                  const std::vector<int>& notToRead) override {
+    if (static_cast<int>(readBufs.size()) != stripeSize() + paritySize() || writeBufs.size() != erased.size())
+      throw std::invalid_argument("decodeBulk: row counts do not match");
+    std::vector<const uint8_t*> in(readBufs.begin(), readBufs.end());
+    check(hrs_decode(h_, in.data(), writeBufs.data(), erased.data(), static_cast<int>(erased.size()),
+                     toRead.data(), static_cast<int>(toRead.size()), notToRead.data(),
+                     static_cast<int>(notToRead.size()), len),
+          h_);
+  }
+
+  // RS-specific decodeBulk(readBufs, writeBufs, erasedLocation), ReedSolomonCode.java:168-185.
+  void decodeBulk3(const std::vector<uint8_t*>& readBufs, const std::vector<uint8_t*>& writeBufs, size_t len,
+                   const std::vector<int>& erased) {
+    std::vector<const uint8_t*> in(readBufs.begin(), readBufs.end());
+    check(hrs_decode3(h_, in.data(), writeBufs.data(), erased.data(), static_cast<int>(erased.size()), len), h_);
+  }
+
+ protected:
+  hrs_codec* h_ = nullptr;
+};
+
+class HipReedSolomonCode : public HipCode {
+ public:
+  HipReedSolomonCode(int stripeSize, int paritySize, int device = -1)
+      : HipCode(HRS_CODE_RS, stripeSize, paritySize, device) {}
+};
+
+class HipXORCode : public HipCode {
+ public:
+  explicit HipXORCode(int stripeSize, int device = -1) : HipCode(HRS_CODE_XOR, stripeSize, 1, device) {}
+};
+
+}  // namespace hrs

@@ -16,6 +16,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#ifdef __cplusplus
+extern "C" {
+#endif
+
 /* GaloisField(256, 285) tables and scalar ops, GaloisField.java:76-204. */
 int orc_gf_mul(int x, int y);
 int orc_gf_div(int x, int y);
@@ -72,5 +76,9 @@ void orc_xor_encode(int k, const int* message, int* parity);
 void orc_xor_decode(int k, const int* data, const int* erased, int ne, int* values);
 void orc_xor_encode_bulk(int k, uint8_t* const* inputs, uint8_t* output, size_t len);
 void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int erased, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
 
 #endif

@@ -1,0 +1,46 @@
+"""The native C++ harness (tests/cpp/codec_harness.cpp) drives libhrs through
+include/hrs.hpp as Encoder.encodeStripe / Decoder.fixErasedBlockImpl drive the
+Java codec: per-bufSize rounds, zlib CRC32 block checksums, the Decoder's
+erased / toRead / notToRead arrays, zero-filled unread inputs; every round is
+checked against the oracle and every repaired block against its stored CRC32."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "tests", "cpp", "codec_harness")
+
+
+def run(*args, timeout=600):
+    if not os.path.exists(HARNESS):
+        subprocess.check_call(["make", "-C", ROOT, "tests/cpp/codec_harness"])
+    out = subprocess.run([HARNESS, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    line = out.stdout.strip().splitlines()[-1]
+    return out.returncode, json.loads(line)
+
+
+@pytest.mark.parametrize("k,p", [(10, 4), (12, 4), (6, 3), (3, 2)])
+def test_harness_host_only(k, p):
+    rc, res = run("--host-only", k, p)
+    assert rc == 0 and res["mismatches"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    (10, 4, 4 << 20, 1 << 20, 1, 3),          # the `rs` codec, 1 MiB bufSize, one lost block
+    (10, 4, 4 << 20, 1 << 20, 4, 5),          # four lost blocks
+    (12, 4, 2 << 20, 256 << 10, 2, 9),        # RS(12,4), 256 KiB cells
+    (6, 3, (3 << 20) + 12345, 1 << 20, 3, 11),  # partial last round (tail bytes)
+    (3, 2, 1 << 20, 1 << 20, 2, 13),
+])
+def test_harness_rs_encoder_decoder(cuda, args):
+    rc, res = run(*args)
+    assert rc == 0 and res["ok"], res
+
+
+@pytest.mark.gpu
+def test_harness_xor(cuda):
+    rc, res = run("--xor", 10, 1, 4 << 20, 1 << 20, 1, 17)
+    assert rc == 0 and res["ok"], res
