@@ -8,10 +8,10 @@ CC       ?= gcc
 
 LIB      := lambdafs_amd/libhrs.so
 ORACLE   := oracle/liboracle.so
-SRCS     := lambdafs_amd/csrc/hrs_api.cpp lambdafs_amd/csrc/hrs_kernels.hip
-HDRS     := include/hrs.h lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp
+HDRS     := include/hrs.h lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
+            lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
 
-HARNESS  := tests/cpp/codec_harness
+HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model
 
 all: $(LIB) $(ORACLE) $(HARNESS)
 
@@ -23,16 +23,23 @@ build/hrs_kernels.o: lambdafs_amd/csrc/hrs_kernels.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): build/hrs_api.o build/hrs_kernels.o
+build/hrs_crc.o: lambdafs_amd/csrc/hrs_crc.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): build/hrs_api.o build/hrs_kernels.o build/hrs_crc.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/rs_oracle.c
 
 # Test-only native harness (tests/cpp): the codec driven like Encoder/Decoder.
-$(HARNESS): tests/cpp/codec_harness.cpp include/hrs.hpp include/hrs.h $(LIB) $(ORACLE)
+tests/cpp/codec_harness: tests/cpp/codec_harness.cpp include/hrs.hpp include/hrs.h $(LIB) $(ORACLE)
 	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs -Loracle -loracle -lz \
 	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
+	g++ -O2 -std=c++17 -Wall -o $@ $< -lz
 
 clean:
 	rm -rf build $(LIB) $(ORACLE) $(HARNESS)

@@ -167,6 +167,15 @@ hrs_status hrs_apply_dev(hrs_codec* codec, const uint8_t* m, int nout, int nin,
                          const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
                          size_t out_stride, size_t len, size_t nstripes, void* stream);
 
+/* CRC-32 of device-resident cells, as java.util.zip.CRC32 (zlib) computes it
+ * for the block checksums the hops drivers keep (Encoder.java:408-450,
+ * Decoder.java:222-229): crc_out[s * nrows + r] = CRC32 of `len` bytes at
+ * rows[r] + s * stride, continuing from crc_in[s * nrows + r] (CRC32.update
+ * chaining across cells; crc_in NULL = a fresh CRC32). crc_in / crc_out are
+ * DEVICE arrays of nstripes * nrows uint32. Asynchronous on `stream`. */
+hrs_status hrs_crc32_dev(hrs_codec* codec, const uint8_t* const* rows, int nrows, size_t stride, size_t len,
+                         size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, void* stream);
+
 /* Kernel selection for tests and benchmarks: 0 = auto (default), 1 = force
  * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel. */
 hrs_status hrs_set_kernel_mode(hrs_codec* codec, int mode);

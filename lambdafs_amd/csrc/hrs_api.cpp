@@ -18,7 +18,9 @@
 #include <vector>
 
 #include "../../include/hrs.h"
+#include "crc32.hpp"
 #include "gf256.hpp"
+#include "hrs_crc.hpp"
 #include "hrs_internal.hpp"
 
 using hrs::RowArgs;
@@ -36,6 +38,11 @@ struct hrs_codec {
   uint8_t* scratch = nullptr;  // device scratch for the host-buffer calls
   size_t scratch_bytes = 0;
   std::map<std::vector<int>, std::vector<uint8_t>> decode_cache;
+  // CRC-32 state (hrs_crc32_dev): fixed window tables, per-length fold tables, scratch
+  uint32_t* crc_tables_a = nullptr;
+  std::map<uint64_t, uint32_t*> crc_fold_tables;
+  uint32_t* crc_raw = nullptr;
+  size_t crc_raw_bytes = 0;
   std::string err;
 };
 
@@ -420,9 +427,125 @@ bool sorted_unique_ok(const int* v, int nv, int n) {
   return true;
 }
 
+// ------------------------------------------------------------------ CRC-32
+
+hrs_status upload(hrs_codec* c, const std::vector<uint32_t>& h, uint32_t** out) {
+  hipError_t e = hipMalloc(out, h.size() * 4);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc: %s", hipGetErrorString(e));
+  e = hipMemcpy(*out, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(c, e, "hipMemcpy tables");
+  return HRS_OK;
+}
+
+hrs_status crc_window_tables(hrs_codec* c) {
+  if (c->crc_tables_a) return HRS_OK;
+  namespace cr = hrs::crc;
+  std::vector<uint32_t> h(hrs::kCrcLdsWordsA);
+  const cr::Slice4 sl = cr::make_slice4();
+  for (int j = 0; j < 4; ++j)
+    for (int v = 0; v < 256; ++v)
+      for (int r = 0; r < hrs::kCrcRep; ++r) h[(j * 256 + v) * hrs::kCrcRep + r] = sl.s[j].t[v];
+  cr::to_tables(cr::zeros(16), &h[hrs::kCrcSliceWords]);  // joins the lane's 16-byte chains
+  for (int t = 0; t < 6; ++t)
+    cr::to_tables(cr::zeros(static_cast<uint64_t>(hrs::kCrcLaneBytes) << t), &h[hrs::kCrcSliceWords + (1 + t) * 1024]);
+  return upload(c, h, &c->crc_tables_a);
+}
+
+hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, const uint32_t** out) {
+  auto it = c->crc_fold_tables.find(len);
+  if (it != c->crc_fold_tables.end()) {
+    *out = it->second;
+    return HRS_OK;
+  }
+  namespace cr = hrs::crc;
+  const uint64_t nwin = len / hrs::kCrcWindow, tail = len % hrs::kCrcWindow;
+  const uint64_t G = (nwin + 63) / 64;
+  std::vector<uint32_t> h(hrs::kCrcLdsWordsB);
+  cr::to_tables(cr::zeros(hrs::kCrcWindow), &h[0]);
+  for (int t = 0; t < 6; ++t) cr::to_tables(cr::zeros(hrs::kCrcWindow * G << t), &h[(1 + t) * 1024]);
+  cr::to_tables(cr::zeros(tail), &h[7 * 1024]);
+  cr::to_tables(cr::zeros(len), &h[8 * 1024]);
+  if (c->crc_fold_tables.size() >= 16) {
+    (void)hipDeviceSynchronize();
+    for (auto& kv : c->crc_fold_tables) (void)hipFree(kv.second);
+    c->crc_fold_tables.clear();
+  }
+  uint32_t* d = nullptr;
+  hrs_status st = upload(c, h, &d);
+  if (st != HRS_OK) return st;
+  c->crc_fold_tables[len] = d;
+  *out = d;
+  return HRS_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+hrs_status hrs_crc32_dev(hrs_codec* c, const uint8_t* const* rows, int nrows, size_t stride, size_t len,
+                         size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!rows || !crc_out || nrows < 1 || nrows > 255) return fail(c, HRS_EINVAL, "bad crc32 arguments");
+  for (int r = 0; r < nrows; ++r)
+    if (!rows[r] && len) return fail(c, HRS_EINVAL, "row %d is NULL", r);
+  if (nstripes == 0) return HRS_OK;
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hrs_status st = crc_window_tables(c);
+  if (st != HRS_OK) return st;
+  const uint32_t* fold = nullptr;
+  st = crc_fold_tables(c, len, &fold);
+  if (st != HRS_OK) return st;
+  const uint64_t nwin = len / hrs::kCrcWindow, tail = len % hrs::kCrcWindow;
+  const uint64_t wpr = nwin + (tail ? 1 : 0);
+  const size_t raw_bytes = std::max<size_t>(4, nstripes * nrows * wpr * 4);
+  if (c->crc_raw_bytes < raw_bytes) {
+    if (c->crc_raw) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(c->crc_raw);
+      c->crc_raw = nullptr;
+      c->crc_raw_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&c->crc_raw, raw_bytes);
+    if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", raw_bytes, hipGetErrorString(e));
+    c->crc_raw_bytes = raw_bytes;
+  }
+  const int cus = hrs::device_cu_count();
+  bool aligned = stride % 16 == 0;
+  for (int r = 0; r < nrows; ++r) aligned &= aligned16(rows[r]);
+  if (wpr > 0) {
+    for (int r0 = 0; r0 < nrows; r0 += hrs::kCrcMaxRows) {
+      hrs::CrcWinArgs a{};
+      a.nrows = std::min(hrs::kCrcMaxRows, nrows - r0);
+      for (int r = 0; r < a.nrows; ++r) a.rows[r] = rows[r0 + r];
+      a.row0 = r0;
+      a.nrows_total = nrows;
+      a.stride = stride;
+      a.len = len;
+      a.nwin = nwin;
+      a.tail = tail;
+      a.nstripes = nstripes;
+      a.raw = c->crc_raw;
+      a.tables = c->crc_tables_a;
+      hipError_t e = hrs::launch_crc_windows(a, aligned, cus, s);
+      if (e != hipSuccess) return hip_fail(c, e, "crc window launch");
+    }
+  }
+  hrs::CrcFoldArgs f{};
+  f.raw = c->crc_raw;
+  f.nwin = nwin;
+  f.tail = tail;
+  f.nsr = nstripes * nrows;
+  f.G = static_cast<int>((nwin + 63) / 64);
+  f.tables = fold;
+  f.crc_in = crc_in;
+  f.crc_out = crc_out;
+  hipError_t e = hrs::launch_crc_fold(f, cus, s);
+  if (e != hipSuccess) return hip_fail(c, e, "crc fold launch");
+  return HRS_OK;
+}
+
 
 const char* hrs_version(void) { return "hrs 0.1.0 (gfx950)"; }
 
@@ -496,6 +619,9 @@ void hrs_destroy(hrs_codec* c) {
     (void)hipStreamDestroy(c->stream);
   }
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->crc_tables_a) (void)hipFree(c->crc_tables_a);
+  for (auto& kv : c->crc_fold_tables) (void)hipFree(kv.second);
+  if (c->crc_raw) (void)hipFree(c->crc_raw);
   delete c;
 }
 

@@ -1,0 +1,187 @@
+// gfx950 CRC-32 (java.util.zip.CRC32 / zlib) of device-resident cells, for the
+// block checksums the hops drivers keep (Encoder.java:408-450,
+// Decoder.java:222-229, :645-655). Two launches:
+//
+//  A. crc_window_kernel: one wave per 4 KiB window of one row of one stripe.
+//     Lane l folds its 64 contiguous bytes (16 words) as four independent
+//     16-byte chains (ILP) with slicing-by-4 tables in LDS — replicated 4x
+//     across banks so random byte indices collide less — joins them with Z_16,
+//     then a 6-level lane tree joins neighbours with zero-append operators
+//     Z_{64*2^t} (crc32.hpp). Lane 0 stores the window's raw CRC.
+//     The row tail (len mod 4 KiB) is a right-aligned window whose leading
+//     bytes are zero (leading zeros do not change a raw CRC).
+//  B. crc_fold_kernel: one wave per (stripe, row) folds its window CRCs
+//     (G per lane with Z_4096, then a lane tree with Z_{4096*G*2^t}), appends
+//     the tail window, and applies CRC32.update's affine chaining from the
+//     running value crc_in.
+// Both are HBM-read streams with LDS-table arithmetic; algorithmic bytes =
+// the rows' bytes, once.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "hrs_crc.hpp"
+
+namespace hrs {
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t wave_id() {
+  return __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6));
+}
+
+// Z(c) from a 4 x 256 table image in LDS.
+__device__ __forceinline__ uint32_t zmul(const uint32_t* z, uint32_t c) {
+  return z[c & 0xFFu] ^ z[256 + ((c >> 8) & 0xFFu)] ^ z[512 + ((c >> 16) & 0xFFu)] ^ z[768 + (c >> 24)];
+}
+
+// One slicing-by-4 step on the replicated tables: lane uses replica `rep`.
+__device__ __forceinline__ uint32_t slice4(const uint32_t* s, uint32_t c, int rep) {
+  constexpr int R = kCrcRep;
+  return s[(3 * 256 + (c & 0xFFu)) * R + rep] ^ s[(2 * 256 + ((c >> 8) & 0xFFu)) * R + rep] ^
+         s[(1 * 256 + ((c >> 16) & 0xFFu)) * R + rep] ^ s[(0 * 256 + (c >> 24)) * R + rep];
+}
+
+template <bool ALIGNED>
+__global__ void __launch_bounds__(256) crc_window_kernel(const CrcWinArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  for (int i = threadIdx.x; i < kCrcLdsWordsA; i += blockDim.x) lds[i] = a.tables[i];
+  __syncthreads();
+  const uint32_t* slices = lds;
+  const uint32_t* z16 = lds + kCrcSliceWords;
+  const uint32_t* tree = z16 + 1024;
+  const int lane = threadIdx.x & 63;
+  const int rep = lane & (kCrcRep - 1);
+  const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
+  const uint64_t ntasks = a.nstripes * a.nrows * wpr;
+  const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+  for (uint64_t t = wave_id(); t < ntasks; t += nwaves) {
+    const uint64_t sr = t / wpr;
+    const uint64_t w = t - sr * wpr;
+    const uint64_t stripe = sr / a.nrows;
+    const int row = static_cast<int>(sr - stripe * a.nrows);
+    const uint8_t* base = a.rows[row] + stripe * a.stride;
+    uint32_t words[16];
+    if (ALIGNED && w < a.nwin) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(base + w * kCrcWindow + lane * kCrcLaneBytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32x4 v = __builtin_nontemporal_load(p + j);
+        words[4 * j] = v[0];
+        words[4 * j + 1] = v[1];
+        words[4 * j + 2] = v[2];
+        words[4 * j + 3] = v[3];
+      }
+    } else {
+      // masked bytes: a full window of an unaligned row, or the right-aligned tail window
+      const int64_t end = (w < a.nwin) ? static_cast<int64_t>((w + 1) * kCrcWindow) : static_cast<int64_t>(a.len);
+      const int64_t lo = (w < a.nwin) ? static_cast<int64_t>(w * kCrcWindow) : static_cast<int64_t>(a.nwin * kCrcWindow);
+      const int64_t start = end - kCrcWindow + lane * kCrcLaneBytes;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int64_t pos = start + 4 * j + b;
+          if (pos >= lo) x |= static_cast<uint32_t>(base[pos]) << (8 * b);
+        }
+        words[j] = x;
+      }
+    }
+    // four independent 16-byte chains, then joined: c = Z16(...Z16(c0) ^ c1 ...) ^ c3
+    uint32_t ch[kCrcChains] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int step = 0; step < 4; ++step)
+#pragma unroll
+      for (int q = 0; q < kCrcChains; ++q) ch[q] = slice4(slices, ch[q] ^ words[4 * q + step], rep);
+    uint32_t c = ch[0];
+#pragma unroll
+    for (int q = 1; q < kCrcChains; ++q) c = zmul(z16, c) ^ ch[q];
+#pragma unroll
+    for (int lvl = 0; lvl < 6; ++lvl) {
+      const uint32_t o = __shfl_down(c, 1 << lvl, 64);
+      c = zmul(tree + lvl * 1024, c) ^ o;
+    }
+    if (lane == 0) a.raw[(stripe * a.nrows_total + a.row0 + row) * wpr + w] = c;
+  }
+}
+
+__global__ void __launch_bounds__(256) crc_fold_kernel(const CrcFoldArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  for (int i = threadIdx.x; i < kCrcLdsWordsB; i += blockDim.x) lds[i] = a.tables[i];
+  __syncthreads();
+  const uint32_t* zw = lds;                    // Z_4096
+  const uint32_t* ztree = lds + 1024;          // Z_{4096*G*2^t}, t = 0..5
+  const uint32_t* ztail = lds + 7 * 1024;      // Z_tail
+  const uint32_t* zlen = lds + 8 * 1024;       // Z_len
+  const int lane = threadIdx.x & 63;
+  const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
+  const uint64_t pad = static_cast<uint64_t>(a.G) * 64 - a.nwin;
+  const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+  for (uint64_t sr = wave_id(); sr < a.nsr; sr += nwaves) {
+    const uint32_t* raw = a.raw + sr * wpr;
+    uint32_t c = 0;
+    for (int g = 0; g < a.G; ++g) {
+      const int64_t w = static_cast<int64_t>(lane) * a.G + g - static_cast<int64_t>(pad);
+      if (w >= 0) c = zmul(zw, c) ^ raw[w];
+    }
+#pragma unroll
+    for (int lvl = 0; lvl < 6; ++lvl) {
+      const uint32_t o = __shfl_down(c, 1 << lvl, 64);
+      c = zmul(ztree + lvl * 1024, c) ^ o;
+    }
+    if (lane == 0) {
+      if (a.tail) c = zmul(ztail, c) ^ raw[a.nwin];
+      const uint32_t state = (a.crc_in ? a.crc_in[sr] : 0u) ^ 0xFFFFFFFFu;
+      a.crc_out[sr] = zmul(zlen, state) ^ c ^ 0xFFFFFFFFu;
+    }
+  }
+}
+
+unsigned grid_for_waves(uint64_t waves, int cus) {
+  static const int per_cu = [] {
+    const char* e = getenv("HRS_CRC_BLOCKS_PER_CU");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 1 && x <= 16) ? x : kCrcBlocksPerCU;
+  }();
+  uint64_t blocks = (waves + 3) / 4;
+  const uint64_t cap = static_cast<uint64_t>(cus) * per_cu;
+  if (blocks > cap) blocks = cap;
+  return static_cast<unsigned>(blocks ? blocks : 1);
+}
+
+}  // namespace
+
+hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStream_t s) {
+  const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
+  const unsigned g = grid_for_waves(a.nstripes * a.nrows * wpr, cus);
+  const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
+  if (aligned) {
+    auto k = crc_window_kernel<true>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(shm));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(g), dim3(256), shm, s, a);
+  } else {
+    auto k = crc_window_kernel<false>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(shm));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(g), dim3(256), shm, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_crc_fold(const CrcFoldArgs& a, int cus, hipStream_t s) {
+  const unsigned g = grid_for_waves(a.nsr, cus);
+  const size_t shm = static_cast<size_t>(kCrcLdsWordsB) * 4;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_fold_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(crc_fold_kernel, dim3(g), dim3(256), shm, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hrs

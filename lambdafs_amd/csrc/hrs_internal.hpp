@@ -49,6 +49,7 @@ enum class KernelKind : int {
 hipError_t launch_static_encode(int k, int p, const RowArgs& a, hipStream_t s, bool* handled);
 hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s);
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s);
-hipError_t launch_xor(const RowArgs& a, hipStream_t s);  // out[0] = XOR of in[0..nin)
+hipError_t launch_xor(const RowArgs& a, hipStream_t s);
+int device_cu_count();  // CUs of the current device (cached)  // out[0] = XOR of in[0..nin)
 
 }  // namespace hrs

@@ -398,6 +398,8 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
 
 }  // namespace
 
+int device_cu_count() { return device_cus(); }
+
 hipError_t launch_static_encode(int k, int p, const RowArgs& a, hipStream_t s, bool* handled) {
   *handled = true;
   if (k == 10 && p == 4) return launch_static<10, 4>(a, s);

@@ -87,3 +87,22 @@ def apply_rows(code, matrix, in_rows, out_rows):
         raise ValueError("shape mismatch")
     code._check(_lib.lib().hrs_apply_dev(code._handle(), m.ctypes.data, m.shape[0], m.shape[1], ins, s_in, outs,
                                          s_out, L, S, _stream(in_rows[0])))
+
+
+def crc32_rows(code, row_views, crc_in=None):
+    """CRC-32 (java.util.zip.CRC32) of every [S, L] row view, per stripe:
+    returns an int32 tensor [S, nrows] holding the uint32 CRC bits
+    (`& 0xFFFFFFFF` for the Java long value). crc_in, if given, is an int32
+    tensor [S, nrows] of running CRCs to continue (CRC32.update chaining)."""
+    torch = _lib.torch
+    rows, stride, L, S = _rows(row_views)
+    ref = next(v for v in row_views if v is not None)
+    out = torch.empty((S, len(row_views)), dtype=torch.int32, device=ref.device)
+    cin = None
+    if crc_in is not None:
+        if crc_in.shape != out.shape or crc_in.dtype != torch.int32 or not crc_in.is_contiguous():
+            raise ValueError("crc_in must be a contiguous int32 tensor [S, nrows]")
+        cin = crc_in.data_ptr()
+    code._check(_lib.lib().hrs_crc32_dev(code._handle(), rows, len(row_views), stride, L, S, cin, out.data_ptr(),
+                                         _stream(ref)))
+    return out

@@ -1,0 +1,103 @@
+// CPU model of the CRC-32 kernels (lambdafs_amd/csrc/hrs_crc.hip): the same
+// tables (crc32.hpp) and the same decomposition — 64 lanes x 64 B slicing-by-4
+// per 4 KiB window (four 16-byte chains per lane joined by Z_16), a 6-level lane tree with Z_{64*2^t}, the window fold with
+// G windows per lane + Z_{4096*G*2^t} tree, the right-aligned tail window and
+// CRC32.update chaining — emulated lane by lane and checked against zlib.
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../lambdafs_amd/csrc/crc32.hpp"
+
+using namespace hrs::crc;
+
+static uint32_t zmul(const std::vector<uint32_t>& z, uint32_t c) {
+  return z[c & 255] ^ z[256 + ((c >> 8) & 255)] ^ z[512 + ((c >> 16) & 255)] ^ z[768 + (c >> 24)];
+}
+static std::vector<uint32_t> tab(uint64_t n) {
+  std::vector<uint32_t> t(1024);
+  to_tables(zeros(n), t.data());
+  return t;
+}
+
+static std::vector<uint32_t> z16 = tab(16);
+
+static uint32_t window_raw(const Slice4& sl, const std::vector<std::vector<uint32_t>>& tree, const uint8_t* p,
+                           int64_t start, int64_t lo, int64_t end) {
+  uint32_t c[64];
+  for (int lane = 0; lane < 64; ++lane) {
+    uint32_t w[16];
+    for (int j = 0; j < 16; ++j) {
+      w[j] = 0;
+      for (int b = 0; b < 4; ++b) {
+        int64_t pos = start + lane * 64 + 4 * j + b;
+        if (pos >= lo && pos < end) w[j] |= (uint32_t)p[pos] << (8 * b);
+      }
+    }
+    uint32_t ch[4] = {0, 0, 0, 0};  // four 16-byte chains, joined with Z_16
+    for (int step = 0; step < 4; ++step)
+      for (int q = 0; q < 4; ++q) {
+        uint32_t x = ch[q] ^ w[4 * q + step];
+        ch[q] = sl.s[3].t[x & 255] ^ sl.s[2].t[(x >> 8) & 255] ^ sl.s[1].t[(x >> 16) & 255] ^ sl.s[0].t[x >> 24];
+      }
+    uint32_t x = ch[0];
+    for (int q = 1; q < 4; ++q) x = zmul(z16, x) ^ ch[q];
+    c[lane] = x;
+  }
+  for (int lvl = 0; lvl < 6; ++lvl) {
+    uint32_t n[64];
+    for (int l = 0; l < 64; ++l) n[l] = zmul(tree[lvl], c[l]) ^ (l + (1 << lvl) < 64 ? c[l + (1 << lvl)] : 0);
+    for (int l = 0; l < 64; ++l) c[l] = n[l];
+  }
+  return c[0];
+}
+
+int main() {
+  const Slice4 sl = make_slice4();
+  std::vector<std::vector<uint32_t>> tree;
+  for (int t = 0; t < 6; ++t) tree.push_back(tab(64ull << t));
+  int bad = 0, cases = 0;
+  uint64_t seed = 1;
+  for (size_t len : {0ul, 1ul, 63ul, 64ul, 4095ul, 4096ul, 4097ul, 8192ul + 5, 65536ul * 3 + 1000, 1ul << 20,
+                     (1ul << 20) + 4096 * 70 + 33}) {
+    std::vector<uint8_t> d(len);
+    for (auto& x : d) x = (uint8_t)((seed = seed * 6364136223846793005ull + 1442695040888963407ull) >> 56);
+    const uint64_t nwin = len / 4096, tail = len % 4096, G = (nwin + 63) / 64;
+    std::vector<uint32_t> raw(nwin + 1);
+    for (uint64_t w = 0; w < nwin; ++w) raw[w] = window_raw(sl, tree, d.data(), w * 4096, w * 4096, (w + 1) * 4096);
+    if (tail) raw[nwin] = window_raw(sl, tree, d.data(), (int64_t)len - 4096, nwin * 4096, len);
+    auto zw = tab(4096), ztail = tab(tail), zlen = tab(len);
+    std::vector<std::vector<uint32_t>> ft;
+    for (int t = 0; t < 6; ++t) ft.push_back(tab(4096 * G << t));
+    for (uint32_t crc_in : {0u, 0xDEADBEEFu}) {
+      uint32_t c[64];
+      const int64_t pad = (int64_t)G * 64 - (int64_t)nwin;
+      for (int l = 0; l < 64; ++l) {
+        c[l] = 0;
+        for (uint64_t g = 0; g < G; ++g) {
+          int64_t w = (int64_t)l * G + g - pad;
+          if (w >= 0) c[l] = zmul(zw, c[l]) ^ raw[w];
+        }
+      }
+      for (int lvl = 0; lvl < 6; ++lvl) {
+        uint32_t n[64];
+        for (int l = 0; l < 64; ++l) n[l] = zmul(ft[lvl], c[l]) ^ (l + (1 << lvl) < 64 ? c[l + (1 << lvl)] : 0);
+        for (int l = 0; l < 64; ++l) c[l] = n[l];
+      }
+      uint32_t r = c[0];
+      if (tail) r = zmul(ztail, r) ^ raw[nwin];
+      const uint32_t out = zmul(zlen, crc_in ^ 0xFFFFFFFFu) ^ r ^ 0xFFFFFFFFu;
+      static const uint8_t one = 0;  // zlib returns 0 for a NULL buffer; CRC32.update(b, 0, 0) keeps the value
+      const uint32_t ref = (uint32_t)crc32(crc_in, len ? d.data() : &one, (uInt)len);
+      ++cases;
+      if (out != ref) {
+        ++bad;
+        printf("len %zu crc_in %08x: model %08x zlib %08x\n", len, crc_in, out, ref);
+      }
+    }
+  }
+  printf("{\"crc_model_cases\": %d, \"mismatches\": %d}\n", cases, bad);
+  return bad ? 1 : 0;
+}

@@ -1,0 +1,88 @@
+"""GPU CRC-32 of device-resident cells (hrs_crc32_dev), bit-exact with
+java.util.zip.CRC32 — the checksum Encoder.java:408-450 keeps per source and
+parity block and Decoder.java:222-229 re-checks after repair. The JDK's CRC32
+is zlib's CRC-32 (the JDK bundles zlib), so Python's zlib.crc32 (system zlib
+1.2.11) is the oracle here."""
+import os
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+from lambdafs_amd import HipReedSolomonCode, device
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_crc_kernel_model_against_zlib():
+    """CPU model of the kernels' decomposition (same tables) vs zlib."""
+    binary = os.path.join(ROOT, "tests", "cpp", "crc_model")
+    if not os.path.exists(binary):
+        subprocess.check_call(["make", "-C", ROOT, "tests/cpp/crc_model"])
+    out = subprocess.run([binary], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
+def _u32(x):
+    return int(x) & 0xFFFFFFFF
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [0, 1, 100, 4095, 4096, 4097, 65536 + 13, 1 << 20, (1 << 20) + 4096 * 70 + 33])
+def test_crc32_rows_match_zlib(cuda, L):
+    torch = cuda
+    code = HipReedSolomonCode(10, 4)
+    S, n = 3, 14
+    g = torch.Generator(device="cuda")
+    g.manual_seed(L + 1)
+    st = torch.randint(0, 256, (S, n, max(L, 1)), dtype=torch.uint8, device="cuda", generator=g)[:, :, :L]
+    crcs = device.crc32_rows(code, [st[:, r, :] for r in range(n)])
+    host = st.cpu().numpy()
+    got = crcs.cpu().numpy()
+    for s in range(S):
+        for r in range(n):
+            assert _u32(got[s, r]) == zlib.crc32(host[s, r].tobytes()), (L, s, r)
+
+
+@pytest.mark.gpu
+def test_crc32_chaining_like_CRC32_update(cuda):
+    """Running block CRC over successive 1 MiB cells == CRC of the block."""
+    torch = cuda
+    code = HipReedSolomonCode(10, 4)
+    block = torch.randint(0, 256, (2, 4 << 20), dtype=torch.uint8, device="cuda")
+    crc = None
+    for off in range(0, 4 << 20, 1 << 20):
+        cells = [block[:, off:off + (1 << 20)]]
+        crc = device.crc32_rows(code, cells, crc)
+    host = block.cpu().numpy()
+    for s in range(2):
+        assert _u32(crc[s, 0]) == zlib.crc32(host[s].tobytes())
+
+
+@pytest.mark.gpu
+def test_crc32_unaligned_rows(cuda):
+    torch = cuda
+    code = HipReedSolomonCode(10, 4)
+    buf = torch.randint(0, 256, (3, 20000), dtype=torch.uint8, device="cuda")
+    view = buf[:, 3:3 + 12345]  # rows start 3 bytes into each 20000-byte line
+    crcs = device.crc32_rows(code, [view])
+    host = view.cpu().numpy()
+    for s in range(3):
+        assert _u32(crcs[s, 0]) == zlib.crc32(host[s].tobytes())
+
+
+@pytest.mark.gpu
+def test_encode_then_block_checksums(cuda):
+    """The Encoder's pattern on device-resident stripes: encode, then CRC32 of
+    every source and parity cell (Encoder.java:434-450)."""
+    torch = cuda
+    k, p, L, S = 10, 4, 1 << 20, 16
+    code = HipReedSolomonCode(k, p)
+    st = torch.randint(0, 256, (S, k + p, L), dtype=torch.uint8, device="cuda")
+    device.encode_stripes(code, st)
+    crcs = device.crc32_rows(code, [st[:, r, :] for r in range(k + p)]).cpu().numpy()
+    host = st.cpu().numpy()
+    for s in (0, S - 1):
+        for r in range(k + p):
+            assert _u32(crcs[s, r]) == zlib.crc32(host[s, r].tobytes())

@@ -199,6 +199,35 @@ __global__ void __launch_bounds__(256) copy_kernel(const u32x4* __restrict__ src
 }
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Probe with W-byte windows: lane owns W/64 bytes of each row as W/1024 16-B pieces
+// (each piece-instruction a coalesced 1 KiB wave access).
+template <int K, int P, int W>
+__global__ void __launch_bounds__(kBlockThreads) probe_wide_kernel(const RowArgs a, uint64_t nwin_w) {
+  constexpr int NP = W / 1024;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint64_t ntasks = nwin_w * (a.ntasks / a.nwin);
+  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
+    const uint64_t stripe = t / nwin_w;
+    const uint64_t off = (t - stripe * nwin_w) * W;
+    u32x4 acc[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) acc[j] = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        acc[j] ^= __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4*>(a.in[r] + stripe * a.in_stride + off + j * 1024 + lane * 16));
+#pragma unroll
+    for (int o = 0; o < P; ++o)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        __builtin_nontemporal_store(acc[j] + (uint32_t)o,
+                                    reinterpret_cast<u32x4*>(a.out[o] + stripe * a.out_stride + off + j * 1024 + lane * 16));
+  }
+}
+
 // Probe with rows staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
 // instruction), then read back with ds_read_b128: is the DMA read path faster?
 template <int K, int P>
@@ -429,6 +458,21 @@ int main(int argc, char** argv) {
     auto pe = encode_static_kernel<10, 4>;
     vars.push_back({"product encode grid=512", [=]() {
                       hipLaunchKernelGGL(pe, dim3(512), dim3(kBlockThreads), 0, 0, a); }, enc_bytes, {}});
+  }
+  if (std::string(which) == "wide") {
+    auto w2 = lab::probe_wide_kernel<10, 4, 2048>;
+    auto w4 = lab::probe_wide_kernel<10, 4, 4096>;
+    auto w8 = lab::probe_wide_kernel<10, 4, 8192>;
+    auto w1 = lab::probe_wide_kernel<10, 4, 1024>;
+    auto pe = encode_static_kernel<10, 4>;
+    for (unsigned g : {256u, 512u, 1024u}) {
+      const std::string t = " grid=" + std::to_string(g);
+      vars.push_back({"wide probe W=1K" + t, [=]() { hipLaunchKernelGGL(w1, dim3(g), dim3(kBlockThreads), 0, 0, a, (uint64_t)(L / 1024)); }, enc_bytes, {}});
+      vars.push_back({"wide probe W=2K" + t, [=]() { hipLaunchKernelGGL(w2, dim3(g), dim3(kBlockThreads), 0, 0, a, (uint64_t)(L / 2048)); }, enc_bytes, {}});
+      vars.push_back({"wide probe W=4K" + t, [=]() { hipLaunchKernelGGL(w4, dim3(g), dim3(kBlockThreads), 0, 0, a, (uint64_t)(L / 4096)); }, enc_bytes, {}});
+      vars.push_back({"wide probe W=8K" + t, [=]() { hipLaunchKernelGGL(w8, dim3(g), dim3(kBlockThreads), 0, 0, a, (uint64_t)(L / 8192)); }, enc_bytes, {}});
+    }
+    vars.push_back({"product encode grid=512", [=]() { hipLaunchKernelGGL(pe, dim3(512), dim3(kBlockThreads), 0, 0, a); }, enc_bytes, {}});
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
