@@ -230,8 +230,9 @@ def main():
                 "algorithmic_bytes_per_launch": enc_bytes,
             },
             "decode_roofline": {
-                "kernel": "bitsliced_kernel<1>", "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
+                "kernel": "bitsliced_kernel<1,12>", "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(dec_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(dec_ms, 4),
+                "traffic": load_traffic("bitsliced_kernel<1,12>"),
                 "algorithmic_bytes_per_launch": dec_bytes,
             },
             "cpu_baseline": None,
