@@ -55,7 +55,14 @@ typedef struct hrs_codec hrs_codec;
  * hadoop-hdfs/src/main/resources/erasure-coding-default.xml:13-56). */
 enum {
   HRS_CODE_RS = 0,  /* "rs":  io.hops.erasure_coding.ReedSolomonCode (ReedSolomonCode.java) */
-  HRS_CODE_XOR = 1  /* "xor": io.hops.erasure_coding.XORCode (XORCode.java), parity_size == 1 */
+  HRS_CODE_XOR = 1, /* "xor": io.hops.erasure_coding.XORCode (XORCode.java), parity_size == 1 */
+  HRS_CODE_NRS = 2  /* "nrs": io.hops.erasure_coding.NativeReedSolomonCode (NativeReedSolomonCode.java)
+                     * over libhadoop's ISA-L shim (erasure_coder.c): Cauchy RS, Apache
+                     * [data, parity] coding order behind the hops [parity, data] locations.
+                     * Decode outputs follow the Java's ordering: output t is the t-th
+                     * not-to-read location in Apache order (needs num_erased <= num_not_to_read
+                     * <= parity_size). No 3-arg decode (hrs_decode3 -> HRS_EINVAL). The
+                     * reference's native limits (k <= 10, k + p <= 14) are lifted. */
 };
 
 #define HRS_DEVICE_NONE (-2)
@@ -73,8 +80,9 @@ typedef struct hrs_opts {
  * parity_size). Requires stripe_size >= 1, parity_size >= 1 and
  * stripe_size + parity_size < 256 (ReedSolomonCode.java:57). opts may be NULL. */
 hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out);
-/* Same for any code family: HRS_CODE_RS (== hrs_create) or HRS_CODE_XOR
- * (XORCode.init asserts parity_size == 1, XORCode.java:46-51). */
+/* Same for any code family: HRS_CODE_RS (== hrs_create), HRS_CODE_XOR
+ * (XORCode.init asserts parity_size == 1, XORCode.java:46-51) or HRS_CODE_NRS
+ * (NativeReedSolomonCode.init, NativeReedSolomonCode.java:44-51). */
 hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts,
                            hrs_codec** out);
 int hrs_code_kind(const hrs_codec* codec);

@@ -139,4 +139,14 @@ class HipXORCode : public HipCode {
   explicit HipXORCode(int stripeSize, int device = -1) : HipCode(HRS_CODE_XOR, stripeSize, 1, device) {}
 };
 
+// NativeReedSolomonCode (the `nrs` codec, ISA-L Cauchy RS); decode outputs in
+// the Java's order (hrs.h, HRS_CODE_NRS). symbolSize and decodeBulk3 throw,
+// as UnsupportedOperationException / no such method in the Java.
+class HipNativeReedSolomonCode : public HipCode {
+ public:
+  HipNativeReedSolomonCode(int stripeSize, int paritySize, int device = -1)
+      : HipCode(HRS_CODE_NRS, stripeSize, paritySize, device) {}
+  int symbolSize() const override { throw std::logic_error("Not supported yet."); }
+};
+
 }  // namespace hrs

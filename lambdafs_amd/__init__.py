@@ -5,9 +5,10 @@ include/hrs.h). This package is its host-side mirror of the reference plugin
 interface (io.hops.erasure_coding.ErasureCode / Codec) plus device-batch
 helpers; every byte is computed on the GPU.
 """
-from .erasure_code import ErasureCode, HipReedSolomonCode, HipXORCode, TooManyErasedLocations  # noqa: F401
+from .erasure_code import (ErasureCode, HipNativeReedSolomonCode, HipReedSolomonCode, HipXORCode,  # noqa: F401
+                           TooManyErasedLocations)  # noqa: F401
 from .codec import Codec, DEFAULT_CODECS_JSON  # noqa: F401
 from ._lib import HrsError  # noqa: F401
 
-__all__ = ["ErasureCode", "HipReedSolomonCode", "HipXORCode", "TooManyErasedLocations", "Codec", "DEFAULT_CODECS_JSON",
+__all__ = ["ErasureCode", "HipReedSolomonCode", "HipXORCode", "HipNativeReedSolomonCode", "TooManyErasedLocations", "Codec", "DEFAULT_CODECS_JSON",
            "HrsError"]

@@ -24,6 +24,7 @@ HRS_EALIGN = 5
 
 HRS_CODE_RS = 0
 HRS_CODE_XOR = 1
+HRS_CODE_NRS = 2
 
 # Every entry point declared in include/hrs.h (checked by tests/test_abi.py).
 EXPORTS = (

@@ -9,7 +9,7 @@ MI355X engine plugs in exactly there: set
 """
 import json
 
-from .erasure_code import HipReedSolomonCode, HipXORCode
+from .erasure_code import HipNativeReedSolomonCode, HipReedSolomonCode, HipXORCode
 
 ERASURE_CODE_KEY_PREFIX = "hdfs.raid.erasure.code."  # Codec.java:52-53
 ERASURE_CODING_CODECS_KEY = "dfs.erasure_coding.codecs.json"  # DFSConfigKeys.java:558
@@ -28,11 +28,12 @@ DEFAULT_CODECS_JSON = json.dumps([
 ])
 
 # Java class name -> implementation available in this engine (the RS hot path
-# and its XOR sibling); any other class resolves to ClassNotFound, as a
+# and its XOR and ISA-L-compatible siblings); any other class resolves to ClassNotFound, as a
 # Java conf naming a missing class would (Codec.java:206-208).
 ERASURE_CODE_CLASSES = {
     HipReedSolomonCode.JAVA_CLASS: HipReedSolomonCode,
     HipXORCode.JAVA_CLASS: HipXORCode,
+    HipNativeReedSolomonCode.JAVA_CLASS: HipNativeReedSolomonCode,
 }
 
 

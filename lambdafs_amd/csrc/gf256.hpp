@@ -126,5 +126,16 @@ struct EncodeMatrix {
   }
 };
 
+// Parity rows of ISA-L gf_gen_cauchy1_matrix(m = K + P, k = K), the nrs code
+// (erasure_coder.c:47-60): m[r][c] = 1 / ((K + r) ^ c).
+template <int K, int P>
+struct CauchyMatrix {
+  uint8_t m[P][K];
+  constexpr CauchyMatrix() : m{} {
+    for (int r = 0; r < P; ++r)
+      for (int c = 0; c < K; ++c) m[r][c] = inv(static_cast<uint8_t>((K + r) ^ c));
+  }
+};
+
 }  // namespace gf
 }  // namespace hrs

@@ -165,6 +165,8 @@ hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const in
   return HRS_OK;
 }
 
+hrs_status build_nrs_decode_matrix(hrs_codec* c, int ne, const int* ntr, int nn, std::vector<uint8_t>& d);
+
 const std::vector<uint8_t>* cached_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
                                                  int zero_ntr, hrs_status* st) {
   std::vector<int> key;
@@ -180,10 +182,64 @@ const std::vector<uint8_t>* cached_decode_matrix(hrs_codec* c, const int* erased
     return &it->second;
   }
   std::vector<uint8_t> d;
-  *st = build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, d);
+  *st = c->kind == HRS_CODE_NRS ? build_nrs_decode_matrix(c, ne, ntr, nn, d)
+                                : build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, d);
   if (*st != HRS_OK) return nullptr;
   if (c->decode_cache.size() > 4096) c->decode_cache.clear();
   return &(c->decode_cache[key] = std::move(d));
+}
+
+// nrs (NativeReedSolomonCode.java:90-152 over erasure_coder.c:102-230): hops
+// location l maps to Apache index a(l) = l + k for parity (l < p), l - p for
+// data. Every not-to-read location is treated as erased; the decoder takes the
+// first k remaining Apache indices as survivors (processErasures), inverts
+// their rows of [I; Cauchy] and emits one row per not-to-read location in
+// ascending Apache order: data rows of the inverse, parity rows = E[e] * inv.
+// The Java copies output i into writeBufs[i] for i < writeBufs.length, so
+// output t decodes the t-th smallest Apache not-to-read index, whichever
+// location erased[t] names (reproduced here, bug-compatibly). Returned as an
+// ne x n matrix over hops locations.
+hrs_status build_nrs_decode_matrix(hrs_codec* c, int ne, const int* ntr, int nn, std::vector<uint8_t>& d) {
+  const int k = c->k, p = c->p, n = c->n;
+  if (nn > p) return fail(c, HRS_EINVAL, "%d not-to-read locations leave fewer than %d survivors", nn, k);
+  if (ne > nn)  // bwriteBufs has |notToRead| entries (NativeReedSolomonCode.java:96,145-149)
+    return fail(c, HRS_EINVAL, "%d erased locations > %d not-to-read locations", ne, nn);
+  std::vector<char> gone(n, 0);
+  std::vector<int> mod(nn);
+  for (int j = 0; j < nn; ++j) {
+    if (ntr[j] < 0 || ntr[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range [0,%d)", ntr[j], n);
+    const int a = ntr[j] < p ? ntr[j] + k : ntr[j] - p;
+    if (gone[a]) return fail(c, HRS_EINVAL, "duplicate location %d", ntr[j]);
+    gone[a] = 1;
+    mod[j] = a;
+  }
+  std::sort(mod.begin(), mod.end());
+  auto erow = [&](int a, int j) -> uint8_t {  // [I; Cauchy] (ISA-L gf_gen_cauchy1_matrix)
+    return a < k ? static_cast<uint8_t>(a == j) : gf::inv(static_cast<uint8_t>(a ^ j));
+  };
+  std::vector<int> idx;
+  for (int a = 0; a < n && static_cast<int>(idx.size()) < k; ++a)
+    if (!gone[a]) idx.push_back(a);
+  std::vector<uint8_t> b(static_cast<size_t>(k) * k);
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) b[i * k + j] = erow(idx[i], j);
+  if (!gf_invert(b, k)) return fail(c, HRS_EINVAL, "singular survivor matrix");
+  d.assign(static_cast<size_t>(ne) * n, 0);
+  for (int t = 0; t < ne; ++t) {
+    const int e = mod[t];
+    for (int i = 0; i < k; ++i) {
+      uint8_t s = 0;
+      if (e < k) {
+        s = b[e * k + i];
+      } else {
+        for (int j = 0; j < k; ++j) s ^= gf::mul(b[j * k + i], erow(e, j));
+      }
+      const int a = idx[i];
+      const int hops = a < k ? a + p : a - k;
+      d[static_cast<size_t>(t) * n + hops] = s;
+    }
+  }
+  return HRS_OK;
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -191,6 +247,7 @@ const std::vector<uint8_t>* cached_decode_matrix(hrs_codec* c, const int* erased
 // The matrix a 5-arg decodeBulk applies (ne x n), per code family.
 //  RS : cached closed-form matrix; more than p not-to-read locations throw in
 //       the Java (errSignature is sized p, ReedSolomonCode.java:60).
+//  NRS: see build_nrs_decode_matrix.
 //  XOR: exactly one erased location; the output is the XOR of every other row
 //       (XORCode.java:115-145 ignores toRead/notToRead). Rows the caller passes
 //       as NULL are the zeros the reference reads there (StripeReader.java:111-120).
@@ -208,7 +265,8 @@ hrs_status decode5_matrix(hrs_codec* c, const int* erased, int ne, const int* nt
     *out = tmp.data();
     return HRS_OK;
   }
-  if (nn > c->p) return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
+  if (c->kind == HRS_CODE_RS && nn > c->p)
+    return fail(c, HRS_EINVAL, "%d not-to-read locations > parity size %d", nn, c->p);
   hrs_status st;
   const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, ntr, nn, 1, &st);
   if (!d) return st;
@@ -272,7 +330,8 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
     a.nin = nin;
     a.nout = nout;
     bool handled = false;
-    hipError_t e = hrs::launch_static_encode(c->k, c->p, a, s, &handled);
+    const int family = c->kind == HRS_CODE_NRS ? hrs::kStaticCauchy : hrs::kStaticRs;
+    hipError_t e = hrs::launch_static_encode(family, c->k, c->p, a, s, &handled);
     if (e != hipSuccess) return hip_fail(c, e, "static encode launch");
     if (handled) {
       if (tail == 0) return HRS_OK;
@@ -310,7 +369,7 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
         RowArgs b = a;
         for (int i = 0; i < ni; ++i) {
           b.in[i] = a.in[i] + tail_off;
-          b.coef[0][i] = 1;
+          hrs::set_coef(b, 0, i, 1);
         }
         b.out[0] = a.out[0] + tail_off;
         b.len = tail;
@@ -331,7 +390,7 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
       for (int i = 0; i < ni; ++i) a.in[i] = in_rows[live[i0 + i]];
       for (int o = 0; o < no; ++o) {
         a.out[o] = out_rows[o0 + o];
-        for (int i = 0; i < ni; ++i) a.coef[o][i] = m[(o0 + o) * nin + live[i0 + i]];
+        for (int i = 0; i < ni; ++i) hrs::set_coef(a, o, i, m[(o0 + o) * nin + live[i0 + i]]);
       }
       a.in_stride = in_stride;
       a.out_stride = out_stride;
@@ -415,9 +474,14 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
 
 void init_encode_matrix(hrs_codec* c) {
   c->g.resize(static_cast<size_t>(c->p) * c->k);
-  if (c->kind == HRS_CODE_XOR)
+  if (c->kind == HRS_CODE_XOR) {
     std::fill(c->g.begin(), c->g.end(), 1);  // XORCode.encodeBulk, XORCode.java:99-113
-  else
+  } else if (c->kind == HRS_CODE_NRS) {
+    // Cauchy rows of ISA-L gf_gen_cauchy1_matrix (erasure_coder.c:47-60):
+    // parity r = Apache row k + r, G[r][c] = 1 / ((k + r) ^ c)
+    for (int r = 0; r < c->p; ++r)
+      for (int j = 0; j < c->k; ++j) c->g[r * c->k + j] = gf::inv(static_cast<uint8_t>((c->k + r) ^ j));
+  } else
     gf::encode_matrix(c->k, c->p, c->g.data());
 }
 
@@ -558,7 +622,7 @@ int hrs_code_kind(const hrs_codec* c) { return c ? c->kind : -1; }
 hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out) {
   if (!out) return fail(nullptr, HRS_EINVAL, "out is NULL");
   *out = nullptr;
-  if (code != HRS_CODE_RS && code != HRS_CODE_XOR) return fail(nullptr, HRS_EINVAL, "unknown code family %d", code);
+  if (code != HRS_CODE_RS && code != HRS_CODE_XOR && code != HRS_CODE_NRS) return fail(nullptr, HRS_EINVAL, "unknown code family %d", code);
   if (code == HRS_CODE_XOR && parity_size != 1)
     return fail(nullptr, HRS_EINVAL, "XOR code needs parity size 1 (XORCode.java:47), got %d", parity_size);
   if (stripe_size < 1 || parity_size < 1 || stripe_size + parity_size >= gf::kFieldSize ||
@@ -670,6 +734,10 @@ hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, con
   if (c->kind == HRS_CODE_XOR) {
     const uint8_t* x = nullptr;
     st = decode5_matrix(c, erased, ne, ntr, nn, nullptr, m, &x);
+  } else if (c->kind == HRS_CODE_NRS) {
+    for (int t = 0; t < ne; ++t)
+      if (erased[t] < 0 || erased[t] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+    st = build_nrs_decode_matrix(c, ne, ntr, nn, m);
   } else {
     st = build_decode_matrix(c, erased, ne, ntr, nn, zero_ntr, m);
   }
@@ -680,7 +748,7 @@ hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, con
 hrs_status hrs_encode(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
   if (!c) return HRS_EINVAL;
   if (!inputs || !outputs) return fail(c, HRS_EINVAL, "inputs/outputs is NULL");
-  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind == HRS_CODE_RS);
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind != HRS_CODE_XOR);
 }
 
 hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
@@ -710,6 +778,8 @@ hrs_status hrs_decode3(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* c
     if (st != HRS_OK) return st;
     return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
   }
+  if (c->kind == HRS_CODE_NRS)  // NativeReedSolomonCode has no 3-arg decodeBulk
+    return fail(c, HRS_EINVAL, "decodeBulk(readBufs, writeBufs, erasedLocations) is not supported by nrs");
   if (ne == 0) return HRS_OK;  // ReedSolomonCode.java:170-172
   if (ne > c->p) return fail(c, HRS_EINVAL, "%d erasures > parity size %d", ne, c->p);  // errSignature[p]
   hrs_status st;
@@ -725,7 +795,7 @@ hrs_status hrs_encode_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   return run_apply(c, c->g.data(), c->p, c->k, in_rows, in_stride, out_rows, out_stride, len, nstripes,
-                   static_cast<hipStream_t>(stream), c->kind == HRS_CODE_RS);
+                   static_cast<hipStream_t>(stream), c->kind != HRS_CODE_XOR);
 }
 
 hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_stride, uint8_t* const* out_rows,

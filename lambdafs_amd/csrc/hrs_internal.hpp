@@ -26,7 +26,7 @@ constexpr int kWavesPerBlock = kBlockThreads / 64;
 struct RowArgs {
   const uint8_t* in[kMaxIn];
   uint8_t* out[kMaxOut];
-  uint8_t coef[kMaxOut][kMaxIn];  // runtime-matrix kernels only
+  uint64_t cw[kMaxIn];            // runtime-matrix kernels: byte o of cw[i] = coefficient (output o, input i)
   uint64_t in_stride;             // bytes between stripes, all input rows
   uint64_t out_stride;            // bytes between stripes, all output rows
   uint64_t len;                   // bytes per row (cell size)
@@ -38,6 +38,10 @@ struct RowArgs {
   int pad_;
 };
 
+inline void set_coef(RowArgs& a, int o, int i, uint8_t v) {
+  a.cw[i] = (a.cw[i] & ~(0xFFull << (8 * o))) | (static_cast<uint64_t>(v) << (8 * o));
+}
+
 enum class KernelKind : int {
   kStaticEncode = 0,   // compile-time encode matrix (3,2) (6,3) (10,4) (12,4)
   kBitsliced = 1,      // runtime matrix, bit-sliced
@@ -46,7 +50,9 @@ enum class KernelKind : int {
 
 // Launches; return hipSuccess or the launch error. `grid_cap` = 0 picks a
 // chip-filling grid from the occupancy API.
-hipError_t launch_static_encode(int k, int p, const RowArgs& a, hipStream_t s, bool* handled);
+// family: kStaticRs (hops generator-polynomial code) or kStaticCauchy (nrs).
+enum { kStaticRs = 0, kStaticCauchy = 1 };
+hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipStream_t s, bool* handled);
 hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s);
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s);
 hipError_t launch_xor(const RowArgs& a, hipStream_t s);

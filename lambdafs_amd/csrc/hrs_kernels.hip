@@ -40,6 +40,12 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// a ^ (b & c) in one VALU op (truth table 0x78): multiply-accumulate of one
+// plane under a 0 / ~0 mask (an SGPR).
+__device__ __forceinline__ uint32_t xor_and(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x78);
+}
+
 // Bitwise select m ? x : y in one VALU op (v_bitop3_b32, truth table 0xCA).
 __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
   return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
@@ -116,20 +122,21 @@ __device__ __forceinline__ uint32_t wave_id_in_grid() {
 
 // mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of
 // parity row o (gf::row_mask of G[o][r]). Evaluated by the compiler.
-template <int K, int P>
+// MATRIX is gf::EncodeMatrix<K,P> (hops RS) or gf::CauchyMatrix<K,P> (nrs).
+template <int K, int P, class MATRIX>
 struct StaticPlan {
   uint8_t mask[P][K][8];
   constexpr StaticPlan() : mask{} {
-    const gf::EncodeMatrix<K, P> g;
+    const MATRIX g;
     for (int o = 0; o < P; ++o)
       for (int r = 0; r < K; ++r)
         for (int q = 0; q < 8; ++q) mask[o][r][q] = gf::row_mask(g.m[o][r], q);
   }
 };
 
-template <int K, int P>
-__global__ void __launch_bounds__(kBlockThreads) encode_static_kernel(const RowArgs a) {
-  constexpr StaticPlan<K, P> plan{};
+template <int K, int P, class MATRIX>
+__device__ __forceinline__ void encode_static_body(const RowArgs& a) {
+  constexpr StaticPlan<K, P, MATRIX> plan{};
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
@@ -184,17 +191,29 @@ __global__ void __launch_bounds__(kBlockThreads) encode_static_kernel(const RowA
   }
 }
 
+template <int K, int P>
+__global__ void __launch_bounds__(kBlockThreads) encode_static_kernel(const RowArgs a) {
+  encode_static_body<K, P, gf::EncodeMatrix<K, P>>(a);
+}
+
+// nrs: the Cauchy rows of ISA-L gf_gen_cauchy1_matrix (NativeReedSolomonCode)
+template <int K, int P>
+__global__ void __launch_bounds__(kBlockThreads) encode_cauchy_kernel(const RowArgs a) {
+  encode_static_body<K, P, gf::CauchyMatrix<K, P>>(a);
+}
+
 // ------------------------------------------ runtime-matrix bit-sliced kernel
 
 // NINB >= nin rows of the window are all loaded before any math (one
 // 20 KiB-class burst per wave, like the static kernel), so a wave keeps
 // nin x 2 KiB in flight; coefficients are wave-uniform kernel arguments.
-template <int NOUT, int NINB>
+template <int NOUT, int NINB, bool MASKED>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const int nin = a.nin;
   for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
+    asm volatile("" : "+s"(nin));
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     const uint64_t in_base = stripe * a.in_stride + off;
@@ -219,14 +238,23 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
     for (int r = 0; r < NINB; ++r) {
       if (r < nin) {
         bitslice(rows[r]);
-        uint32_t c[NOUT];
-#pragma unroll
-        for (int o = 0; o < NOUT; ++o) c[o] = a.coef[o][r];
+        // one wave-uniform 64-bit word per input: byte o = coefficient of output o
+        // (kernel arguments: scalar loads; split in halves, no 64-bit shifts).
+        // The empty asm makes them opaque per task so the 8 x NOUT x NINB
+        // masks are not hoisted out of the task loop (they would spill).
+        uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
+        asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
 #pragma unroll
           for (int o = 0; o < NOUT; ++o) {
-            if ((c[o] >> b) & 1u) {
+            const uint32_t bit = (cw[o >> 2] >> (8 * (o & 3) + b)) & 1u;
+            if constexpr (MASKED) {
+              // branch-free: acc ^= (alpha^b x) & (bit ? ~0 : 0), one v_bitop3 per plane
+              const uint32_t m = 0u - bit;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) acc[o][q] = xor_and(acc[o][q], rows[r][q], m);
+            } else if (bit) {
 #pragma unroll
               for (int q = 0; q < 8; ++q) acc[o][q] ^= rows[r][q];
             }
@@ -306,7 +334,7 @@ __global__ void __launch_bounds__(kBlockThreads) bytewise_kernel(const RowArgs a
       const int lx = s_log[x];
 #pragma unroll
       for (int o = 0; o < kMaxOut; ++o) {
-        const uint8_t c = a.coef[o][r];
+        const uint8_t c = static_cast<uint8_t>(a.cw[r] >> (8 * o));
         if (o < a.nout && c != 0) acc[o] ^= s_exp[lx + s_log[c]];
       }
     }
@@ -378,9 +406,25 @@ hipError_t launch_static(const RowArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int K, int P>
+hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
+  auto kern = encode_cauchy_kernel<K, P>;
+  const unsigned g = stream_grid(a.ntasks);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+bool masked_runtime() {
+  static const bool m = [] {
+    const char* e = getenv("HRS_RUNTIME_BRANCHY");
+    return !(e && atoi(e) == 1);
+  }();
+  return m;
+}
+
 template <int NOUT, int NINB>
 hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
-  auto kern = bitsliced_kernel<NOUT, NINB>;
+  auto kern = masked_runtime() ? bitsliced_kernel<NOUT, NINB, true> : bitsliced_kernel<NOUT, NINB, false>;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }
@@ -400,8 +444,14 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
 
 int device_cu_count() { return device_cus(); }
 
-hipError_t launch_static_encode(int k, int p, const RowArgs& a, hipStream_t s, bool* handled) {
+hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipStream_t s, bool* handled) {
   *handled = true;
+  if (family == kStaticCauchy) {
+    if (k == 10 && p == 4) return launch_cauchy<10, 4>(a, s);
+    if (k == 6 && p == 3) return launch_cauchy<6, 3>(a, s);
+    *handled = false;
+    return hipSuccess;
+  }
   if (k == 10 && p == 4) return launch_static<10, 4>(a, s);
   if (k == 6 && p == 3) return launch_static<6, 3>(a, s);
   if (k == 3 && p == 2) return launch_static<3, 2>(a, s);

@@ -375,6 +375,43 @@ class HipXORCode(_HipErasureCode):
         erasedValues[0] = int(out[0][0])
 
 
+class HipNativeReedSolomonCode(_HipErasureCode):
+    """Drop-in for NativeReedSolomonCode (the `nrs` codec,
+    hops-erasure-coding/.../NativeReedSolomonCode.java:32-196), which runs
+    libhadoop's ISA-L coder (erasure_coder.c): a Cauchy RS code
+    (gf_gen_cauchy1_matrix) in Apache [data, parity] order behind the hops
+    [parity, data] locations. Bulk calls only; the scalar methods and
+    symbolSize throw in the Java (UnsupportedOperationException), and so
+    do they here (NotImplementedError).
+
+    decodeBulk keeps the Java's output ordering: writeBufs[t] receives the
+    t-th not-to-read location in Apache order (NativeReedSolomonCode.java:
+    138-149), which is erasedLocations[t] whenever the erased locations are
+    the not-to-read ones, in that order. Inputs are left untouched.
+    """
+
+    CODE_KIND = _lib.HRS_CODE_NRS
+    JAVA_CLASS = "io.hops.erasure_coding.HipNativeReedSolomonCode"
+
+    def encode(self, message, parity):
+        raise NotImplementedError("Not supported yet.")
+
+    def decode(self, data, erasedLocations, erasedValues, locationsToRead=None, locationsNotToRead=None):
+        raise NotImplementedError("Not supported yet.")
+
+    def symbolSize(self):
+        raise NotImplementedError("Not supported yet.")
+
+    def decodeBulk(self, readBufs, writeBufs, erasedLocations, locationsToRead=None, locationsNotToRead=None):
+        """NativeReedSolomonCode.decodeBulk (NativeReedSolomonCode.java:90-152)."""
+        if locationsNotToRead is None:
+            raise NotImplementedError("NativeReedSolomonCode has no 3-argument decodeBulk")
+        if len(writeBufs) > len(locationsNotToRead):
+            # bwriteBufs holds |locationsNotToRead| buffers (NativeReedSolomonCode.java:96, :145-149)
+            raise IndexError("more write buffers than not-to-read locations")
+        super().decodeBulk(readBufs, writeBufs, erasedLocations, locationsToRead, locationsNotToRead)
+
+
 def _symbol(v):
     v = int(v)
     if not 0 <= v < 256:

@@ -10,6 +10,7 @@ import java.io.IOException;
 final class HrsNative {
   static final int CODE_RS = 0;   // HRS_CODE_RS
   static final int CODE_XOR = 1;  // HRS_CODE_XOR
+  static final int CODE_NRS = 2;  // HRS_CODE_NRS
 
   static {
     System.loadLibrary("hrs_jni");  // libhrs_jni.so -> libhrs.so

@@ -409,3 +409,128 @@ void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int 
     for (size_t j = 0; j < len; j++) output[j] ^= input[j];
   }
 }
+
+/* ------------------------------------------------- nrs (ISA-L Cauchy RS) */
+
+/* ISA-L gf_mul / gf_inv over 0x11D: the same field as GaloisField (285). */
+static int isal_mul(int a, int b) { return mulTable[a][b]; }
+static int isal_inv(int a) { return a == 0 ? 0 : divTable[1][a]; }
+
+/* ISA-L gf_gen_cauchy1_matrix(a, m, k): identity on top, then a[i][j] = 1/(i ^ j). */
+void orc_nrs_encode_matrix(int k, int p, uint8_t* a) {
+  int m = k + p;
+  memset(a, 0, (size_t)k * m);
+  for (int i = 0; i < k; i++) a[k * i + i] = 1;
+  uint8_t* q = &a[k * k];
+  for (int i = k; i < m; i++)
+    for (int j = 0; j < k; j++) *q++ = (uint8_t)isal_inv(i ^ j);
+}
+
+/* ISA-L gf_invert_matrix(in, out, n): Gauss-Jordan; returns -1 if singular. */
+static int isal_invert(uint8_t* in, uint8_t* out, int n) {
+  memset(out, 0, (size_t)n * n);
+  for (int i = 0; i < n; i++) out[i * n + i] = 1;
+  for (int i = 0; i < n; i++) {
+    if (in[i * n + i] == 0) {
+      int j;
+      for (j = i + 1; j < n; j++)
+        if (in[j * n + i]) break;
+      if (j == n) return -1;
+      for (int t = 0; t < n; t++) {
+        uint8_t x = in[i * n + t]; in[i * n + t] = in[j * n + t]; in[j * n + t] = x;
+        x = out[i * n + t]; out[i * n + t] = out[j * n + t]; out[j * n + t] = x;
+      }
+    }
+    int piv = isal_inv(in[i * n + i]);
+    for (int t = 0; t < n; t++) {
+      in[i * n + t] = (uint8_t)isal_mul(in[i * n + t], piv);
+      out[i * n + t] = (uint8_t)isal_mul(out[i * n + t], piv);
+    }
+    for (int j = 0; j < n; j++) {
+      if (j == i) continue;
+      int f = in[j * n + i];
+      for (int t = 0; t < n; t++) {
+        out[j * n + t] ^= (uint8_t)isal_mul(f, out[i * n + t]);
+        in[j * n + t] ^= (uint8_t)isal_mul(f, in[i * n + t]);
+      }
+    }
+  }
+  return 0;
+}
+
+/* ISA-L ec_encode_data: dest[r][b] = XOR_j rows[r][j] * src[j][b]. */
+static void isal_encode(size_t len, int ksrc, int rows, const uint8_t* mat, uint8_t* const* src, uint8_t* const* dst) {
+  for (int r = 0; r < rows; r++)
+    for (size_t b = 0; b < len; b++) {
+      int s = 0;
+      for (int j = 0; j < ksrc; j++) s ^= isal_mul(mat[r * ksrc + j], src[j][b]);
+      dst[r][b] = (uint8_t)s;
+    }
+}
+
+/* NativeReedSolomonCode.encodeBulk (NativeReedSolomonCode.java:55-88) ->
+ * erasure_coder.c encode (:66-80): parity = Cauchy rows x data. */
+void orc_nrs_encode_bulk(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  uint8_t* a = (uint8_t*)malloc((size_t)(k + p) * k);
+  orc_nrs_encode_matrix(k, p, a);
+  isal_encode(len, k, p, a + k * k, inputs, outputs);
+  free(a);
+}
+
+static int cmp_int(const void* x, const void* y) { return *(const int*)x - *(const int*)y; }
+
+/* NativeReedSolomonCode.decodeBulk (NativeReedSolomonCode.java:90-152): hops
+ * [parity, data] -> Apache [data, parity]; every not-to-read location is NULL
+ * and "erased" (sorted Apache order); erasure_coder.c processErasures
+ * (:106-156) + generateDecodeMatrix (:189-230) + ec_encode_data; then
+ * writeBufs[i] = the i-th decoded output (sorted Apache order), i < ne. */
+int orc_nrs_decode_bulk(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                        int ne, const int* not_to_read, int nn, size_t len) {
+  (void)erased;
+  int m = k + p;
+  uint8_t** in = (uint8_t**)calloc((size_t)m, sizeof(uint8_t*));
+  for (int i = 0; i < p; i++) in[i + k] = read_bufs[i];
+  for (int i = 0; i < k; i++) in[i] = read_bufs[i + p];
+  int* mod = (int*)malloc(sizeof(int) * (size_t)(nn > 0 ? nn : 1));
+  for (int i = 0; i < nn; i++) {
+    int loc = not_to_read[i];
+    if (loc < p) { in[loc + k] = NULL; mod[i] = loc + k; }
+    else { in[loc - p] = NULL; mod[i] = loc - p; }
+  }
+  qsort(mod, (size_t)nn, sizeof(int), cmp_int);
+  /* processErasures: decodeIndex = first k non-NULL inputs */
+  int* decodeIndex = (int*)malloc(sizeof(int) * (size_t)k);
+  int r = 0;
+  for (int i = 0; i < k; i++, r++) {
+    while (r < m && in[r] == NULL) r++;
+    if (r >= m) { free(in); free(mod); free(decodeIndex); return -1; }
+    decodeIndex[i] = r;
+  }
+  uint8_t* enc = (uint8_t*)malloc((size_t)m * k);
+  orc_nrs_encode_matrix(k, p, enc);
+  uint8_t* tmp = (uint8_t*)malloc((size_t)k * k);
+  uint8_t* inv = (uint8_t*)malloc((size_t)k * k);
+  for (int i = 0; i < k; i++)
+    for (int j = 0; j < k; j++) tmp[k * i + j] = enc[k * decodeIndex[i] + j];
+  int st = isal_invert(tmp, inv, k);
+  int nErasedData = 0;
+  for (int i = 0; i < nn; i++) if (mod[i] < k) nErasedData++;
+  uint8_t* dec = (uint8_t*)calloc((size_t)(nn > 0 ? nn : 1) * k, 1);
+  for (int i = 0; i < nErasedData; i++)
+    for (int j = 0; j < k; j++) dec[k * i + j] = inv[k * mod[i] + j];
+  for (int q = nErasedData; q < nn; q++)
+    for (int i = 0; i < k; i++) {
+      int s = 0;
+      for (int j = 0; j < k; j++) s ^= isal_mul(inv[j * k + i], enc[k * mod[q] + j]);
+      dec[k * q + i] = (uint8_t)s;
+    }
+  uint8_t** real = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)k);
+  for (int i = 0; i < k; i++) real[i] = in[decodeIndex[i]];
+  uint8_t** outs = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)(nn > 0 ? nn : 1));
+  for (int i = 0; i < nn; i++) outs[i] = (uint8_t*)calloc(len ? len : 1, 1);
+  isal_encode(len, k, nn, dec, real, outs);
+  for (int i = 0; i < ne && i < nn; i++) memcpy(write_bufs[i], outs[i], len);
+  for (int i = 0; i < nn; i++) free(outs[i]);
+  free(outs); free(real); free(dec); free(inv); free(tmp); free(enc); free(decodeIndex); free(mod); free(in);
+  return st;
+}

@@ -77,6 +77,16 @@ void orc_xor_decode(int k, const int* data, const int* erased, int ne, int* valu
 void orc_xor_encode_bulk(int k, uint8_t* const* inputs, uint8_t* output, size_t len);
 void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int erased, size_t len);
 
+/* NativeReedSolomonCode (the `nrs` codec, hops-erasure-coding/.../NativeReedSolomonCode.java)
+ * over libhadoop's ISA-L shim (hadoop-common/src/main/native/src/org/apache/hadoop/io/
+ * erasurecode/erasure_coder.c) and ISA-L (absent here, version unpinned: restated from its
+ * published gf_gen_cauchy1_matrix / gf_invert_matrix / ec_encode_data definitions).
+ * Rows in hops order [parity, data]; read_bufs entries may be NULL (not read). */
+void orc_nrs_encode_matrix(int k, int p, uint8_t* a /* (k+p) x k, ISA-L layout */);
+void orc_nrs_encode_bulk(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len);
+int orc_nrs_decode_bulk(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                        int ne, const int* not_to_read, int nn, size_t len);
+
 #ifdef __cplusplus
 }
 #endif

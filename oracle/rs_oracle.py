@@ -63,6 +63,9 @@ def lib():
             "orc_xor_decode": ([I, IP, IP, I, IP], None),
             "orc_xor_encode_bulk": ([I, PP, ctypes.c_void_p, S], None),
             "orc_xor_decode_bulk": ([I, PP, ctypes.c_void_p, I, S], None),
+            "orc_nrs_encode_matrix": ([I, I, ctypes.c_void_p], None),
+            "orc_nrs_encode_bulk": ([I, I, PP, PP, S], None),
+            "orc_nrs_decode_bulk": ([I, I, PP, PP, IP, I, IP, I, S], I),
         }
         for name, (args, res) in sigs.items():
             f = getattr(_lib, name)
@@ -237,6 +240,31 @@ def xor_decode_bulk(k, read_bufs, erased):
     out = np.zeros(rows[0].size, dtype=np.uint8)
     lib().orc_xor_decode_bulk(k, _rowptrs(rows), out.ctypes.data, int(erased), out.size)
     return out
+
+
+# ------------------------------------------------- nrs (ISA-L Cauchy RS)
+
+def nrs_encode_matrix(k, p):
+    a = np.zeros((k + p, k), dtype=np.uint8)
+    lib().orc_nrs_encode_matrix(k, p, a.ctypes.data)
+    return a
+
+
+def nrs_encode_bulk(k, p, inputs):
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    outs = [np.zeros(rows[0].size, dtype=np.uint8) for _ in range(p)]
+    lib().orc_nrs_encode_bulk(k, p, _rowptrs(rows), _rowptrs(outs), rows[0].size)
+    return outs
+
+
+def nrs_decode_bulk(k, p, read_bufs, erased, not_to_read):
+    rows = [None if r is None else np.ascontiguousarray(r, dtype=np.uint8) for r in read_bufs]
+    L = max(r.size for r in rows if r is not None)
+    outs = [np.zeros(L, dtype=np.uint8) for _ in erased]
+    st = lib().orc_nrs_decode_bulk(k, p, _rowptrs(rows), _rowptrs(outs), _ints(erased), len(erased),
+                                   _ints(not_to_read), len(not_to_read), L)
+    assert st == 0
+    return outs
 
 
 # Raw entry points for the CPU baseline (pointer arrays prepared once).

@@ -11,7 +11,11 @@
 //    (StripeReader.java:106-124); code.decodeBulk(...) per round (:352-353);
 //    the repaired block's CRC32 compared with the stored one (:222-229).
 //
-// Usage: codec_harness [--host-only] [--xor] k p blockSize bufSize nerased seed
+// Usage: codec_harness [--host-only] [--xor | --nrs] k p blockSize bufSize nerased seed
+// --nrs drives NativeReedSolomonCode semantics: rounds are checked against the
+// oracle's orc_nrs_decode_bulk, and the repaired CRC against the block the Java
+// actually returns in writeBufs[i] (the i-th not-to-read location in Apache
+// order; "quirk" says whether that differs from erasedLocations[i]).
 // Prints one JSON line; exit status 0 iff everything matched.
 #include <zlib.h>
 
@@ -75,7 +79,7 @@ int host_only_checks(int k, int p) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  bool host_only = false, use_xor = false;
+  bool host_only = false, use_xor = false, use_nrs = false;
   std::vector<std::string> pos;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -83,6 +87,8 @@ int main(int argc, char** argv) {
       host_only = true;
     else if (a == "--xor")
       use_xor = true;
+    else if (a == "--nrs")
+      use_nrs = true;
     else
       pos.push_back(a);
   }
@@ -99,6 +105,8 @@ int main(int argc, char** argv) {
     std::unique_ptr<hrs::HipCode> code;
     if (use_xor)
       code.reset(new hrs::HipXORCode(k, 0));
+    else if (use_nrs)
+      code.reset(new hrs::HipNativeReedSolomonCode(k, p, 0));
     else
       code.reset(new hrs::HipReedSolomonCode(k, p, 0));
 
@@ -133,6 +141,8 @@ int main(int argc, char** argv) {
       for (int r = 0; r < p; ++r) refp[r] = ref[r].data();
       if (use_xor)
         orc_xor_encode_bulk(k, cpp.data(), refp[0], len);
+      else if (use_nrs)
+        orc_nrs_encode_bulk(k, p, cpp.data(), refp.data(), len);
       else
         orc_rs_encode_bulk(k, p, cpp.data(), refp.data(), len);
       for (int r = 0; r < p; ++r) {
@@ -171,6 +181,19 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> rep_crc(erased_arr.size(), 0);
     size_t rep_mismatch = 0;
     const int ne = static_cast<int>(erased_arr.size());
+    // the block writeBufs[i] receives: erased_arr[i], or for nrs the i-th
+    // not-to-read location in Apache [data, parity] order
+    std::vector<int> expect(erased_arr);
+    bool quirk = false;
+    if (use_nrs) {
+      std::vector<int> ap;
+      for (int loc : ntr_arr) ap.push_back(loc < p ? loc + k : loc - p);
+      std::sort(ap.begin(), ap.end());
+      for (int i = 0; i < ne; ++i) {
+        expect[i] = ap[i] < k ? ap[i] + p : ap[i] - k;
+        quirk |= expect[i] != erased_arr[i];
+      }
+    }
     std::vector<std::vector<uint8_t>> wb(ne, std::vector<uint8_t>(buf));
     for (size_t off = 0; off < block; off += buf) {
       const size_t len = std::min(buf, block - off);
@@ -186,23 +209,32 @@ int main(int argc, char** argv) {
       code->decodeBulk(rp, wp, len, erased_arr, to_read_arr, ntr_arr);
       t_codec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       for (int i = 0; i < ne; ++i) {
-        rep_mismatch += std::memcmp(wb[i].data(), stripe_row(erased_arr[i]) + off, len) != 0;
+        rep_mismatch += std::memcmp(wb[i].data(), stripe_row(expect[i]) + off, len) != 0;
         rep_crc[i] = crc(rep_crc[i], wb[i].data(), len);
+      }
+      if (use_nrs) {  // the reference's own output for this round
+        std::vector<std::vector<uint8_t>> ref(ne, std::vector<uint8_t>(len));
+        std::vector<uint8_t*> refp(ne);
+        for (int i = 0; i < ne; ++i) refp[i] = ref[i].data();
+        if (orc_nrs_decode_bulk(k, p, rp.data(), refp.data(), erased_arr.data(), ne, ntr_arr.data(),
+                                static_cast<int>(ntr_arr.size()), len) != 0)
+          ++rep_mismatch;
+        for (int i = 0; i < ne; ++i) rep_mismatch += std::memcmp(ref[i].data(), wb[i].data(), len) != 0;
       }
     }
     size_t crc_bad = 0;
     for (int i = 0; i < ne; ++i) {
-      const int loc = erased_arr[i];
+      const int loc = expect[i];
       const uint32_t stored = loc < p ? par_crc[loc] : src_crc[loc - p];  // checksums sent to the NN
       crc_bad += stored != rep_crc[i];
     }
     const bool ok = mismatches == 0 && rep_mismatch == 0 && crc_bad == 0;
-    printf("{\"code\": \"%s\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"erased\": [", use_xor ? "xor" : "rs",
+    printf("{\"code\": \"%s\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"erased\": [", use_xor ? "xor" : use_nrs ? "nrs" : "rs",
            k, p, block, buf);
     for (int i = 0; i < ne; ++i) printf("%s%d", i ? ", " : "", erased_arr[i]);
-    printf("], \"encode_round_mismatches\": %zu, \"repair_mismatches\": %zu, \"crc_mismatches\": %zu, "
+    printf("], \"quirk\": %s, \"encode_round_mismatches\": %zu, \"repair_mismatches\": %zu, \"crc_mismatches\": %zu, "
            "\"codec_seconds\": %.4f, \"ok\": %s}\n",
-           mismatches, rep_mismatch, crc_bad, t_codec, ok ? "true" : "false");
+           quirk ? "true" : "false", mismatches, rep_mismatch, crc_bad, t_codec, ok ? "true" : "false");
     return ok ? 0 : 1;
   } catch (const std::exception& e) {
     printf("{\"error\": \"%s\", \"ok\": false}\n", e.what());

@@ -44,3 +44,13 @@ def test_harness_rs_encoder_decoder(cuda, args):
 def test_harness_xor(cuda):
     rc, res = run("--xor", 10, 1, 4 << 20, 1 << 20, 1, 17)
     assert rc == 0 and res["ok"], res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nerased,seed", [(1, 3), (1, 4), (2, 5), (3, 6), (4, 7), (4, 8)])
+def test_harness_nrs(cuda, nerased, seed):
+    # NativeReedSolomonCode semantics: every round equals the oracle's
+    # orc_nrs_decode_bulk, and each repaired block's CRC equals the stored CRC
+    # of the block the Java hands back (res["quirk"]: not the erased one)
+    rc, res = run("--nrs", 10, 4, 3 << 20, 1 << 20, nerased, seed)
+    assert rc == 0 and res["ok"], res

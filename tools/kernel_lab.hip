@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(kBlockThreads) probe_kernel(const RowArgs a) {
 // The product's static encode body with load/store policy knobs.
 template <int K, int P, bool NT>
 __global__ void __launch_bounds__(kBlockThreads) encode_var_kernel(const RowArgs a) {
-  constexpr StaticPlan<K, P> plan{};
+  constexpr StaticPlan<K, P, gf::EncodeMatrix<K, P>> plan{};
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_old_kernel(const RowA
       bitslice(cur);
       uint32_t c[NOUT];
 #pragma unroll
-      for (int o = 0; o < NOUT; ++o) c[o] = a.coef[o][r];
+      for (int o = 0; o < NOUT; ++o) c[o] = static_cast<uint8_t>(a.cw[r] >> (8 * o));
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
 #pragma unroll
@@ -359,10 +359,10 @@ int main(int argc, char** argv) {
   {
     RowArgs d = a;  // decode 1 erasure through the runtime kernels
     d.nout = 1;
-    for (int c = 0; c < k; ++c) d.coef[0][c] = (uint8_t)(17 * c + 3);
+    for (int c = 0; c < k; ++c) set_coef(d, 0, c, (uint8_t)(17 * c + 3));
     d.out[0] = copy_dst;
     d.out_stride = L;
-    auto knew = bitsliced_kernel<1, 12>;
+    auto knew = bitsliced_kernel<1, 12, true>;
     auto kold = lab::bitsliced_old_kernel<1>;
     for (unsigned g : {512u, 768u, 1024u, 2048u}) {
       vars.push_back({"product bitsliced<1,12> (decode) grid=" + std::to_string(g), [=]() {
@@ -392,12 +392,12 @@ int main(int argc, char** argv) {
     const int locs[10] = {3, 5, 6, 7, 8, 9, 10, 11, 12, 13};
     for (int c = 0; c < k; ++c) {
       d.in[c] = buf + (size_t)locs[c] * L;
-      d.coef[0][c] = (uint8_t)(17 * c + 3);
+      set_coef(d, 0, c, (uint8_t)(17 * c + 3));
     }
     d.out[0] = copy_dst;
     d.out_stride = L;
     auto kenc = encode_static_kernel<10, 4>;
-    auto kdec = bitsliced_kernel<1, 12>;
+    auto kdec = bitsliced_kernel<1, 12, true>;
     for (unsigned g : {512u, 768u}) {
       vars.push_back({"PAIR encode+decode(loc3) dec grid=" + std::to_string(g), [=]() {
                         hipLaunchKernelGGL(kenc, dim3(512), dim3(kBlockThreads), 0, 0, a);
@@ -411,7 +411,7 @@ int main(int argc, char** argv) {
   if (std::string(which) == "pitch") {
     // row pitch sweep: rows at buf + (stripe * n + r) * (L + pad); buffer sized for the max pad
     auto kenc = encode_static_kernel<10, 4>;
-    auto kdec = bitsliced_kernel<1, 12>;
+    auto kdec = bitsliced_kernel<1, 12, true>;
     auto kread = lab::probe_kernel<10, 1, true>;
     for (size_t pad : {(size_t)0, (size_t)256, (size_t)2048, (size_t)4096, (size_t)6144, (size_t)8192,
                        (size_t)12288, (size_t)65536 + 2048}) {
@@ -423,7 +423,7 @@ int main(int argc, char** argv) {
       e.in_stride = e.out_stride = (uint64_t)n * P;
       RowArgs d = e;
       d.nout = 1;
-      for (int c = 0; c < k; ++c) d.coef[0][c] = (uint8_t)(17 * c + 3);
+      for (int c = 0; c < k; ++c) set_coef(d, 0, c, (uint8_t)(17 * c + 3));
       d.out[0] = copy_dst;
       d.out_stride = P;
       const std::string t = " pad=" + std::to_string(pad);
