@@ -168,6 +168,21 @@ hrs_status hrs_decode_dev(hrs_codec* codec, const uint8_t* const* rows, size_t i
                           int num_erased, const int* not_to_read, int num_not_to_read, size_t len,
                           size_t nstripes, void* stream);
 
+/* Repair of a batch whose stripes lost different locations (a repair job over
+ * many stripes: Decoder.fixErasedBlockImpl / recoverBlock per stripe,
+ * Decoder.java:291-338), in one launch. Stripe s holds location l at
+ * stripes + s * stripe_stride + l * row_stride (hops order). Its erased
+ * locations are erased[s * max_erased + t] for t < max_erased up to the first
+ * negative entry (zero erasures allowed). Each stripe is decoded like
+ * hrs_decode_dev with the survivors locationsToReadForDecode picks and every
+ * other location not read (Decoder.java:303-338); output t of stripe s goes to
+ * out + s * out_stripe_stride + t * out_row_stride. HRS_ETOOMANY if a stripe
+ * lost more than the code repairs. */
+hrs_status hrs_decode_batch_dev(hrs_codec* codec, const uint8_t* stripes, size_t row_stride,
+                                size_t stripe_stride, const int* erased, int max_erased, uint8_t* out,
+                                size_t out_row_stride, size_t out_stripe_stride, size_t len,
+                                size_t nstripes, void* stream);
+
 /* Generic GF(2^8) matrix x rows: out_o = XOR_i m[o * nin + i] * in_i (m on
  * the host, row-major nout x nin). Used with coding matrices broadcast over
  * RCCL, and by the 3-arg decode. nin, nout in [1, 255]. */

@@ -32,7 +32,8 @@ EXPORTS = (
     "hrs_stripe_size", "hrs_parity_size", "hrs_symbol_size",
     "hrs_locations_to_read", "hrs_encode_matrix", "hrs_decode_matrix",
     "hrs_encode", "hrs_decode", "hrs_decode3",
-    "hrs_encode_dev", "hrs_decode_dev", "hrs_apply_dev", "hrs_crc32_dev", "hrs_set_kernel_mode",
+    "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
+    "hrs_set_kernel_mode",
 )
 
 
@@ -82,6 +83,7 @@ def lib():
         "hrs_decode3": ([P, PP, PP, IP, I, S], I),
         "hrs_encode_dev": ([P, PP, S, PP, S, S, S, P], I),
         "hrs_decode_dev": ([P, PP, S, PP, S, IP, I, IP, I, S, S, P], I),
+        "hrs_decode_batch_dev": ([P, P, S, S, P, I, P, S, S, S, S, P], I),
         "hrs_apply_dev": ([P, U8P, I, I, PP, S, PP, S, S, S, P], I),
         "hrs_crc32_dev": ([P, PP, I, S, S, S, P, P, P], I),
         "hrs_set_kernel_mode": ([P, I], I),

@@ -43,6 +43,17 @@ struct hrs_codec {
   std::map<uint64_t, uint32_t*> crc_fold_tables;
   uint32_t* crc_raw = nullptr;
   size_t crc_raw_bytes = 0;
+  // hrs_decode_batch_dev: two slots (plans + per-stripe pattern index), each
+  // a device buffer and its pinned staging; a slot is reused once the event
+  // recorded after its launches has completed.
+  struct BatchSlot {
+    uint8_t* dev = nullptr;
+    uint8_t* host = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+  } batch[2];
+  int batch_next = 0;
   std::string err;
 };
 
@@ -686,6 +697,14 @@ void hrs_destroy(hrs_codec* c) {
   if (c->crc_tables_a) (void)hipFree(c->crc_tables_a);
   for (auto& kv : c->crc_fold_tables) (void)hipFree(kv.second);
   if (c->crc_raw) (void)hipFree(c->crc_raw);
+  for (auto& b : c->batch) {
+    if (b.done) {
+      (void)hipEventSynchronize(b.done);
+      (void)hipEventDestroy(b.done);
+    }
+    if (b.dev) (void)hipFree(b.dev);
+    if (b.host) (void)hipHostFree(b.host);
+  }
   delete c;
 }
 
@@ -813,6 +832,150 @@ hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_st
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   return run_apply(c, d, ne, c->n, rows, in_stride, out_rows, out_stride, len, nstripes,
                    static_cast<hipStream_t>(stream), false);
+}
+
+hrs_status hrs_decode_batch_dev(hrs_codec* c, const uint8_t* stripes, size_t row_stride, size_t stripe_stride,
+                                const int* erased, int max_erased, uint8_t* out, size_t out_row_stride,
+                                size_t out_stripe_stride, size_t len, size_t nstripes, void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!stripes || !out || max_erased < 0 || max_erased > hrs::kMaxOut || (max_erased > 0 && !erased))
+    return fail(c, HRS_EINVAL, "bad batch decode arguments (max_erased must be in [0, %d])", hrs::kMaxOut);
+  if (nstripes == 0 || len == 0 || max_erased == 0) return HRS_OK;
+  if (nstripes > 0x7fffffffu) return fail(c, HRS_EINVAL, "too many stripes");
+  // distinct patterns -> plans
+  std::map<std::vector<int>, int> ids;
+  std::vector<int32_t> pat(nstripes);
+  std::vector<hrs::BatchPlan> plans;
+  std::vector<std::vector<uint8_t>> mats;  // per pattern: ne x n decode matrix
+  bool fused = true;
+  int max_nout = 0, max_nin = 0;
+  std::vector<int> key, to_read(c->k), ntr;
+  for (size_t s = 0; s < nstripes; ++s) {
+    key.clear();
+    for (int t = 0; t < max_erased && erased[s * max_erased + t] >= 0; ++t) key.push_back(erased[s * max_erased + t]);
+    auto it = ids.find(key);
+    if (it != ids.end()) {
+      pat[s] = it->second;
+      continue;
+    }
+    const int ne = static_cast<int>(key.size());
+    for (int e : key)
+      if (e >= c->n) return fail(c, HRS_EINVAL, "stripe %zu: erased location %d out of range", s, e);
+    hrs::BatchPlan pl{};
+    std::vector<uint8_t> m(static_cast<size_t>(ne) * c->n, 0);
+    if (ne > 0) {
+      hrs_status st = hrs_locations_to_read(c, key.data(), ne, to_read.data());
+      if (st != HRS_OK) return st;
+      ntr.clear();
+      for (int l = 0; l < c->n; ++l)
+        if (std::find(to_read.begin(), to_read.end(), l) == to_read.end()) ntr.push_back(l);
+      std::vector<uint8_t> tmp;
+      const uint8_t* d = nullptr;
+      st = decode5_matrix(c, key.data(), ne, ntr.data(), static_cast<int>(ntr.size()), nullptr, tmp, &d);
+      if (st != HRS_OK) return st;
+      std::memcpy(m.data(), d, m.size());
+      for (int l = 0; l < c->n; ++l) {
+        bool live = false;
+        for (int o = 0; o < ne; ++o) live |= m[static_cast<size_t>(o) * c->n + l] != 0;
+        if (!live) continue;
+        if (pl.nin < hrs::kBatchMaxIn) {
+          pl.loc[pl.nin] = l;
+          for (int o = 0; o < ne; ++o)
+            pl.cw[pl.nin] |= static_cast<uint64_t>(m[static_cast<size_t>(o) * c->n + l]) << (8 * o);
+        }
+        ++pl.nin;
+      }
+    }
+    pl.nout = ne;
+    if (pl.nin > hrs::kBatchMaxIn || (ne > 5 && pl.nin > hrs::kMaxInRuntimeWide)) fused = false;
+    max_nout = std::max(max_nout, ne);
+    max_nin = std::max(max_nin, pl.nin);
+    const int id = static_cast<int>(plans.size());
+    ids.emplace(key, id);
+    plans.push_back(pl);
+    mats.push_back(std::move(m));
+    pat[s] = id;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  hipStream_t hs = static_cast<hipStream_t>(stream);
+  if (max_nout == 0) return HRS_OK;
+
+  if (!fused) {
+    // shapes beyond the fused kernel (wide codes): one launch per stripe
+    std::vector<const uint8_t*> rows(c->n);
+    std::vector<uint8_t*> outs(hrs::kMaxOut);
+    for (size_t s = 0; s < nstripes; ++s) {
+      const hrs::BatchPlan& pl = plans[pat[s]];
+      if (pl.nout == 0) continue;
+      for (int l = 0; l < c->n; ++l) rows[l] = stripes + s * stripe_stride + l * row_stride;
+      for (int o = 0; o < pl.nout; ++o) outs[o] = out + s * out_stripe_stride + o * out_row_stride;
+      hrs_status st = run_apply(c, mats[pat[s]].data(), pl.nout, c->n, rows.data(), 0, outs.data(), 0, len, 1, hs, false);
+      if (st != HRS_OK) return st;
+    }
+    return HRS_OK;
+  }
+
+  // upload plans + pattern indices through the next slot
+  const size_t plan_bytes = plans.size() * sizeof(hrs::BatchPlan);
+  const size_t need = plan_bytes + nstripes * sizeof(int32_t);
+  hrs_codec::BatchSlot& sl = c->batch[c->batch_next];
+  c->batch_next ^= 1;
+  if (sl.pending) {
+    hipError_t e = hipEventSynchronize(sl.done);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
+    sl.pending = false;
+  }
+  if (!sl.done) {
+    hipError_t e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+  }
+  if (sl.bytes < need) {
+    if (sl.dev) (void)hipFree(sl.dev);
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.dev = nullptr;
+    sl.host = nullptr;
+    sl.bytes = 0;
+    const size_t bytes = std::max<size_t>(need, 64 << 10);
+    hipError_t e = hipMalloc(&sl.dev, bytes);
+    if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    e = hipHostMalloc(&sl.host, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    sl.bytes = bytes;
+  }
+  std::memcpy(sl.host, plans.data(), plan_bytes);
+  std::memcpy(sl.host + plan_bytes, pat.data(), nstripes * sizeof(int32_t));
+  hipError_t e = hipMemcpyAsync(sl.dev, sl.host, need, hipMemcpyHostToDevice, hs);
+  if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync plans");
+
+  hrs::BatchArgs a{};
+  a.base = stripes;
+  a.out = out;
+  a.row_stride = row_stride;
+  a.stripe_stride = stripe_stride;
+  a.out_row_stride = out_row_stride;
+  a.out_stripe_stride = out_stripe_stride;
+  a.len = len;
+  a.plans = reinterpret_cast<const hrs::BatchPlan*>(sl.dev);
+  a.pat = reinterpret_cast<const int32_t*>(sl.dev + plan_bytes);
+  const bool vec = c->kernel_mode != 2 && aligned16(stripes) && aligned16(out) && row_stride % 16 == 0 &&
+                   stripe_stride % 16 == 0 && out_row_stride % 16 == 0 && out_stripe_stride % 16 == 0;
+  a.nwin = vec ? len / hrs::kWindowBytes : 0;
+  if (a.nwin > 0) {
+    a.ntasks = a.nwin * nstripes;
+    e = hrs::launch_batch_bitsliced(a, max_nout, max_nin, hs);
+    if (e != hipSuccess) return hip_fail(c, e, "batch launch");
+  }
+  a.col0 = a.nwin * hrs::kWindowBytes;
+  if (a.col0 < len) {
+    a.ntasks = (len - a.col0) * nstripes;
+    e = hrs::launch_batch_bytewise(a, hs);
+    if (e != hipSuccess) return hip_fail(c, e, "batch bytewise launch");
+  }
+  e = hipEventRecord(sl.done, hs);
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  sl.pending = true;
+  return HRS_OK;
 }
 
 hrs_status hrs_apply_dev(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,

@@ -56,6 +56,31 @@ hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipS
 hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s);
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s);
 hipError_t launch_xor(const RowArgs& a, hipStream_t s);
-int device_cu_count();  // CUs of the current device (cached)  // out[0] = XOR of in[0..nin)
+int device_cu_count();  // CUs of the current device (cached)
+
+// ---- heterogeneous batches: one erasure pattern per stripe (hrs_decode_batch_dev)
+
+constexpr int kBatchMaxIn = 16;
+struct BatchPlan {            // one erasure pattern, a device table entry
+  int nin;                    // live survivor rows read
+  int nout;                   // erased rows written
+  int loc[kBatchMaxIn];       // hops location of input r
+  uint64_t cw[kBatchMaxIn];   // byte o of cw[r] = coefficient (output o, input r)
+};
+
+struct BatchArgs {
+  const uint8_t* base;        // location l of stripe s at base + s * stripe_stride + l * row_stride
+  uint8_t* out;               // output t of stripe s at out + s * out_stripe_stride + t * out_row_stride
+  uint64_t row_stride, stripe_stride, out_row_stride, out_stripe_stride;
+  uint64_t len;               // bytes per row
+  uint64_t col0;              // first byte column this launch covers (tails: nwin * 2048)
+  uint64_t nwin;              // full 2 KiB windows per row (vector kernel)
+  uint64_t ntasks;            // vector: nstripes * nwin; bytewise: nstripes * (len - col0)
+  const BatchPlan* plans;     // device table
+  const int32_t* pat;         // device: pattern index of each stripe
+};
+
+hipError_t launch_batch_bitsliced(const BatchArgs& a, int max_nout, int max_nin, hipStream_t s);
+hipError_t launch_batch_bytewise(const BatchArgs& a, hipStream_t s);
 
 }  // namespace hrs

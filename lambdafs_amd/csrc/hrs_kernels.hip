@@ -40,12 +40,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// a ^ (b & c) in one VALU op (truth table 0x78): multiply-accumulate of one
-// plane under a 0 / ~0 mask (an SGPR).
-__device__ __forceinline__ uint32_t xor_and(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x78);
-}
-
 // Bitwise select m ? x : y in one VALU op (v_bitop3_b32, truth table 0xCA).
 __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
   return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
@@ -207,7 +201,25 @@ __global__ void __launch_bounds__(kBlockThreads) encode_cauchy_kernel(const RowA
 // NINB >= nin rows of the window are all loaded before any math (one
 // 20 KiB-class burst per wave, like the static kernel), so a wave keeps
 // nin x 2 KiB in flight; coefficients are wave-uniform kernel arguments.
-template <int NOUT, int NINB, bool MASKED>
+// Bit loop unrolled (xtime is then a free relabel of the planes) unless the
+// body would outgrow the instruction cache: unrolled, bitsliced<4,12> is
+// 28 KiB of branchy code and ran 40% slower than rolled.
+template <int NOUT, int NINB>
+struct BitLoop {
+  static constexpr bool kRolled = NOUT * NINB >= 40;
+};
+
+template <int NOUT, int NINB>
+__device__ __forceinline__ void mul_acc_row(uint32_t (&acc)[NOUT][8], uint32_t (&x)[8], const uint32_t (&cw)[2], int b) {
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o)
+    if ((cw[o >> 2] >> (8 * (o & 3) + b)) & 1u) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] ^= x[q];
+    }
+}
+
+template <int NOUT, int NINB>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
@@ -238,28 +250,24 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
     for (int r = 0; r < NINB; ++r) {
       if (r < nin) {
         bitslice(rows[r]);
-        // one wave-uniform 64-bit word per input: byte o = coefficient of output o
-        // (kernel arguments: scalar loads; split in halves, no 64-bit shifts).
-        // The empty asm makes them opaque per task so the 8 x NOUT x NINB
-        // masks are not hoisted out of the task loop (they would spill).
+        // one wave-uniform 64-bit word per input (byte o = coefficient of
+        // output o), split in halves; the empty asm keeps the per-(o, b)
+        // tests from being hoisted out of the task loop (they would spill).
         uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
         asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-#pragma unroll
-          for (int o = 0; o < NOUT; ++o) {
-            const uint32_t bit = (cw[o >> 2] >> (8 * (o & 3) + b)) & 1u;
-            if constexpr (MASKED) {
-              // branch-free: acc ^= (alpha^b x) & (bit ? ~0 : 0), one v_bitop3 per plane
-              const uint32_t m = 0u - bit;
-#pragma unroll
-              for (int q = 0; q < 8; ++q) acc[o][q] = xor_and(acc[o][q], rows[r][q], m);
-            } else if (bit) {
-#pragma unroll
-              for (int q = 0; q < 8; ++q) acc[o][q] ^= rows[r][q];
-            }
+        // acc[o] ^= sum over set bits b of coef[o][r]: alpha^b * row
+        if constexpr (BitLoop<NOUT, NINB>::kRolled) {
+#pragma unroll 1
+          for (int b = 0; b < 8; ++b) {
+            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+            xtime(rows[r]);
           }
-          if (b < 7) xtime(rows[r]);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+            if (b < 7) xtime(rows[r]);
+          }
         }
       }
     }
@@ -344,6 +352,102 @@ __global__ void __launch_bounds__(kBlockThreads) bytewise_kernel(const RowArgs a
   }
 }
 
+// ------------------------------- heterogeneous batches (one pattern per stripe)
+
+// Plans and pattern indices are read through the constant address space so
+// the per-task reads are scalar loads (s_load), not vector memory traffic.
+typedef const __attribute__((address_space(4))) BatchPlan* ConstPlanPtr;
+typedef const __attribute__((address_space(4))) int32_t* ConstIntPtr;
+
+// Same arithmetic as bitsliced_kernel; the wave reads its stripe's plan
+// (inputs, coefficients, output count) at the start of each task.
+template <int NOUT, int NINB>
+__global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const BatchArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const ConstPlanPtr plans = (ConstPlanPtr)a.plans;
+  const ConstIntPtr pat = (ConstIntPtr)a.pat;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const ConstPlanPtr pl = plans + pat[stripe];
+    const int nin = pl->nin;
+    const int nout = pl->nout;
+    const uint8_t* sb = a.base + stripe * a.stripe_stride + off;
+    uint32_t rows[NINB][8];
+#pragma unroll
+    for (int r = 0; r < NINB; ++r)
+      if (r < nin) load_row(sb + static_cast<uint64_t>(pl->loc[r]) * a.row_stride, lane, rows[r]);
+    uint32_t acc[NOUT][8];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+#pragma unroll
+    for (int r = 0; r < NINB; ++r) {
+      if (r < nin) {
+        bitslice(rows[r]);
+        const uint64_t w = pl->cw[r];
+        uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
+        asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
+        if constexpr (BitLoop<NOUT, NINB>::kRolled) {
+#pragma unroll 1
+          for (int b = 0; b < 8; ++b) {
+            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+            xtime(rows[r]);
+          }
+        } else {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+            if (b < 7) xtime(rows[r]);
+          }
+        }
+      }
+    }
+    uint8_t* ob = a.out + stripe * a.out_stripe_stride + off;
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      if (o < nout) {
+        bitslice(acc[o]);
+        store_row(ob + static_cast<uint64_t>(o) * a.out_row_stride, lane, acc[o]);
+      }
+    }
+  }
+}
+
+// Byte columns [col0, len) of every stripe (tails, unaligned batches).
+__global__ void __launch_bounds__(kBlockThreads) batch_bytewise_kernel(const BatchArgs a) {
+  __shared__ uint8_t s_exp[512];
+  __shared__ uint8_t s_log[256];
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) s_exp[i] = d_tables.exp[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_log[i] = d_tables.log[i];
+  __syncthreads();
+  const uint64_t ncol = a.len - a.col0;
+  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t idx = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; idx < a.ntasks;
+       idx += nthreads) {
+    const uint64_t stripe = idx / ncol;
+    const uint64_t col = a.col0 + (idx - stripe * ncol);
+    const BatchPlan& pl = a.plans[a.pat[stripe]];
+    const uint8_t* sb = a.base + stripe * a.stripe_stride + col;
+    uint8_t acc[kMaxOut] = {};
+    for (int r = 0; r < pl.nin; ++r) {
+      const uint8_t x = sb[static_cast<uint64_t>(pl.loc[r]) * a.row_stride];
+      if (x == 0) continue;
+      const int lx = s_log[x];
+      const uint64_t w = pl.cw[r];
+#pragma unroll
+      for (int o = 0; o < kMaxOut; ++o) {
+        const uint8_t c = static_cast<uint8_t>(w >> (8 * o));
+        if (c != 0) acc[o] ^= s_exp[lx + s_log[c]];
+      }
+    }
+    uint8_t* ob = a.out + stripe * a.out_stripe_stride + col;
+    for (int o = 0; o < pl.nout; ++o) ob[static_cast<uint64_t>(o) * a.out_row_stride] = acc[o];
+  }
+}
+
 // ------------------------------------------------------------ launching
 
 struct DeviceInfo {
@@ -414,17 +518,9 @@ hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-bool masked_runtime() {
-  static const bool m = [] {
-    const char* e = getenv("HRS_RUNTIME_BRANCHY");
-    return !(e && atoi(e) == 1);
-  }();
-  return m;
-}
-
 template <int NOUT, int NINB>
 hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
-  auto kern = masked_runtime() ? bitsliced_kernel<NOUT, NINB, true> : bitsliced_kernel<NOUT, NINB, false>;
+  auto kern = bitsliced_kernel<NOUT, NINB>;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }
@@ -440,9 +536,47 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+template <int NOUT, int NINB>
+hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
+  auto kern = batch_bitsliced_kernel<NOUT, NINB>;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NOUT>
+hipError_t launch_batch_nout(const BatchArgs& a, int max_nin, hipStream_t s) {
+  if (max_nin <= 4) return launch_batch_n<NOUT, 4>(a, s);
+  if (max_nin <= 8) return launch_batch_n<NOUT, 8>(a, s);
+  if constexpr (NOUT < 6) {
+    if (max_nin <= 12) return launch_batch_n<NOUT, 12>(a, s);
+    if (max_nin <= 16) return launch_batch_n<NOUT, 16>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 int device_cu_count() { return device_cus(); }
+
+hipError_t launch_batch_bitsliced(const BatchArgs& a, int max_nout, int max_nin, hipStream_t s) {
+  switch (max_nout) {
+    case 1: return launch_batch_nout<1>(a, max_nin, s);
+    case 2: return launch_batch_nout<2>(a, max_nin, s);
+    case 3: return launch_batch_nout<3>(a, max_nin, s);
+    case 4: return launch_batch_nout<4>(a, max_nin, s);
+    case 5: return launch_batch_nout<5>(a, max_nin, s);
+    case 6: return launch_batch_nout<6>(a, max_nin, s);
+    case 7: return launch_batch_nout<7>(a, max_nin, s);
+    case 8: return launch_batch_nout<8>(a, max_nin, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_batch_bytewise(const BatchArgs& a, hipStream_t s) {
+  const unsigned g = grid_for(batch_bytewise_kernel, kBlockThreads, a.ntasks);
+  hipLaunchKernelGGL(batch_bytewise_kernel, dim3(g), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipStream_t s, bool* handled) {
   *handled = true;

@@ -77,6 +77,26 @@ def decode_stripes(code, stripes, erased, not_to_read, out):
         int_array(not_to_read), len(not_to_read), L, S, _stream(stripes)))
 
 
+def decode_batch(code, stripes, erased, out):
+    """Repair every stripe of stripes[S, n, L] from its own erasure list, in one
+    launch (hrs_decode_batch_dev): erased is an int array [S, E] of hops
+    locations (ascending per stripe, -1 padded; a row of -1 = nothing lost);
+    out[S, E, L] receives stripe s's repaired rows in that order. Survivors are
+    the ones locationsToReadForDecode picks, as Decoder.fixErasedBlockImpl does."""
+    n = code.stripeSize() + code.paritySize()
+    if stripes.dim() != 3 or stripes.shape[1] != n or stripes.stride(2) != 1:
+        raise ValueError(f"stripes must be [S, {n}, L] with unit byte stride")
+    e = np.ascontiguousarray(np.asarray(erased, dtype=np.int32))
+    S, L = stripes.shape[0], stripes.shape[2]
+    if e.ndim != 2 or e.shape[0] != S:
+        raise ValueError("erased must be [S, E]")
+    if out.dim() != 3 or tuple(out.shape) != (S, e.shape[1], L) or out.stride(2) != 1 or out.device != stripes.device:
+        raise ValueError("out must be [S, E, L] on the stripes' device")
+    code._check(_lib.lib().hrs_decode_batch_dev(
+        code._handle(), stripes.data_ptr(), stripes.stride(1), stripes.stride(0), e.ctypes.data, e.shape[1],
+        out.data_ptr(), out.stride(1), out.stride(0), L, S, _stream(stripes)))
+
+
 def apply_rows(code, matrix, in_rows, out_rows):
     """out_o = XOR_i matrix[o, i] * in_i over S stripes (matrix: host uint8 [nout, nin]).
     Used with coding matrices broadcast over RCCL (bench.py --gpus N)."""

@@ -362,7 +362,7 @@ int main(int argc, char** argv) {
     for (int c = 0; c < k; ++c) set_coef(d, 0, c, (uint8_t)(17 * c + 3));
     d.out[0] = copy_dst;
     d.out_stride = L;
-    auto knew = bitsliced_kernel<1, 12, true>;
+    auto knew = bitsliced_kernel<1, 12>;
     auto kold = lab::bitsliced_old_kernel<1>;
     for (unsigned g : {512u, 768u, 1024u, 2048u}) {
       vars.push_back({"product bitsliced<1,12> (decode) grid=" + std::to_string(g), [=]() {
@@ -397,7 +397,7 @@ int main(int argc, char** argv) {
     d.out[0] = copy_dst;
     d.out_stride = L;
     auto kenc = encode_static_kernel<10, 4>;
-    auto kdec = bitsliced_kernel<1, 12, true>;
+    auto kdec = bitsliced_kernel<1, 12>;
     for (unsigned g : {512u, 768u}) {
       vars.push_back({"PAIR encode+decode(loc3) dec grid=" + std::to_string(g), [=]() {
                         hipLaunchKernelGGL(kenc, dim3(512), dim3(kBlockThreads), 0, 0, a);
@@ -411,7 +411,7 @@ int main(int argc, char** argv) {
   if (std::string(which) == "pitch") {
     // row pitch sweep: rows at buf + (stripe * n + r) * (L + pad); buffer sized for the max pad
     auto kenc = encode_static_kernel<10, 4>;
-    auto kdec = bitsliced_kernel<1, 12, true>;
+    auto kdec = bitsliced_kernel<1, 12>;
     auto kread = lab::probe_kernel<10, 1, true>;
     for (size_t pad : {(size_t)0, (size_t)256, (size_t)2048, (size_t)4096, (size_t)6144, (size_t)8192,
                        (size_t)12288, (size_t)65536 + 2048}) {
