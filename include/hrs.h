@@ -56,6 +56,12 @@ typedef struct hrs_codec hrs_codec;
 enum {
   HRS_CODE_RS = 0,  /* "rs":  io.hops.erasure_coding.ReedSolomonCode (ReedSolomonCode.java) */
   HRS_CODE_XOR = 1, /* "xor": io.hops.erasure_coding.XORCode (XORCode.java), parity_size == 1 */
+  HRS_CODE_SRC = 3, /* "src": io.hops.erasure_coding.SimpleRegeneratingCode (SimpleRegeneratingCode.java):
+                     * RS(k, r) plus s local XOR parities; create with hrs_create_src.
+                     * Locations [SRC parities 0..s-1, RS parities s..p-1, data p..k+p-1].
+                     * Variable-length locationsToReadForDecode (hrs_locations_to_read_list);
+                     * a one-erasure decode XORs the locations to read (device calls: every
+                     * location outside not_to_read); no 3-arg decode. */
   HRS_CODE_NRS = 2  /* "nrs": io.hops.erasure_coding.NativeReedSolomonCode (NativeReedSolomonCode.java)
                      * over libhadoop's ISA-L shim (erasure_coder.c): Cauchy RS, Apache
                      * [data, parity] coding order behind the hops [parity, data] locations.
@@ -86,6 +92,14 @@ hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hr
 hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts,
                            hrs_codec** out);
 int hrs_code_kind(const hrs_codec* codec);
+/* SimpleRegeneratingCode.init(Codec) (SimpleRegeneratingCode.java:52-114):
+ * src_parity_size = the codec's "parity_length_src" (the adjustment loop of
+ * init may lower it; hrs_src_layout reports what it settled on). */
+hrs_status hrs_create_src(int stripe_size, int parity_size, int src_parity_size, const hrs_opts* opts,
+                          hrs_codec** out);
+/* SRC layout after init: stored SRC parities s, RS parities r = p - s, and
+ * the group degree d (locations per stored SRC group). */
+hrs_status hrs_src_layout(const hrs_codec* codec, int* src_parities, int* rs_parities, int* group_degree);
 void hrs_destroy(hrs_codec* codec);
 /* Last error message of this handle ("" if none); handle may be NULL for create errors. */
 const char* hrs_last_error(const hrs_codec* codec);
@@ -97,6 +111,14 @@ int hrs_parity_size(const hrs_codec* codec);
 int hrs_symbol_size(const hrs_codec* codec);
 
 /* ---- host helpers (no device work) ---- */
+
+/* locationsToReadForDecode as a list of variable length, for every code
+ * family (SRC returns a local group; the others exactly stripe_size
+ * locations, as hrs_locations_to_read): to_read has room for k + p entries,
+ * *num_to_read receives the count. SimpleRegeneratingCode.java:300-366,
+ * ErasureCode.java:89-113. */
+hrs_status hrs_locations_to_read_list(const hrs_codec* codec, const int* erased, int num_erased, int* to_read,
+                                      int* num_to_read);
 
 /* ErasureCode.locationsToReadForDecode (ErasureCode.java:89-113): writes the
  * k = stripe_size highest-index locations not in `erased` to to_read, in

@@ -58,7 +58,7 @@ class ErasureCode {
                           const std::vector<int>& locationsToRead,
                           const std::vector<int>& locationsNotToRead) = 0;
   // ErasureCode.java:89-113 — the k highest-index locations not erased, highest first.
-  std::vector<int> locationsToReadForDecode(const std::vector<int>& erasedLocations) const {
+  virtual std::vector<int> locationsToReadForDecode(const std::vector<int>& erasedLocations) const {
     std::vector<int> out;
     const int limit = stripeSize() + paritySize();
     for (int loc = limit - 1; loc >= 0; --loc) {
@@ -81,11 +81,11 @@ class ErasureCode {
 // Common owner of an hrs_codec handle.
 class HipCode : public ErasureCode {
  public:
-  HipCode(int code, int k, int p, int device = -1) {
+  HipCode(int code, int k, int p, int device = -1, int srcParities = 0) {
     hrs_opts o{};
     o.device = device;
     hrs_codec* c = nullptr;
-    hrs_status st = hrs_create_code(code, k, p, &o, &c);
+    hrs_status st = code == HRS_CODE_SRC ? hrs_create_src(k, p, srcParities, &o, &c) : hrs_create_code(code, k, p, &o, &c);
     if (st != HRS_OK) check(st, nullptr);
     h_ = c;
   }
@@ -97,6 +97,17 @@ class HipCode : public ErasureCode {
   int paritySize() const override { return hrs_parity_size(h_); }
   int symbolSize() const override { return hrs_symbol_size(h_); }
   hrs_codec* handle() const { return h_; }
+
+  // the product's list (hrs_locations_to_read_list): SRC returns a local group
+  std::vector<int> locationsToReadForDecode(const std::vector<int>& erasedLocations) const override {
+    std::vector<int> out(stripeSize() + paritySize());
+    int m = 0;
+    check(hrs_locations_to_read_list(h_, erasedLocations.data(), static_cast<int>(erasedLocations.size()), out.data(),
+                                     &m),
+          h_);
+    out.resize(m);
+    return out;
+  }
 
   void encodeBulk(const std::vector<uint8_t*>& inputs, const std::vector<uint8_t*>& outputs, size_t len) override {
     if (static_cast<int>(inputs.size()) != stripeSize() || static_cast<int>(outputs.size()) != paritySize())
@@ -142,6 +153,14 @@ class HipXORCode : public HipCode {
 // NativeReedSolomonCode (the `nrs` codec, ISA-L Cauchy RS); decode outputs in
 // the Java's order (hrs.h, HRS_CODE_NRS). symbolSize and decodeBulk3 throw,
 // as UnsupportedOperationException / no such method in the Java.
+// SimpleRegeneratingCode (the `src` codec): RS(k, r) + stored local XOR
+// parities; srcParities = the codec's "parity_length_src".
+class HipSimpleRegeneratingCode : public HipCode {
+ public:
+  HipSimpleRegeneratingCode(int stripeSize, int paritySize, int srcParities, int device = -1)
+      : HipCode(HRS_CODE_SRC, stripeSize, paritySize, device, srcParities) {}
+};
+
 class HipNativeReedSolomonCode : public HipCode {
  public:
   HipNativeReedSolomonCode(int stripeSize, int paritySize, int device = -1)

@@ -25,10 +25,12 @@ HRS_EALIGN = 5
 HRS_CODE_RS = 0
 HRS_CODE_XOR = 1
 HRS_CODE_NRS = 2
+HRS_CODE_SRC = 3
 
 # Every entry point declared in include/hrs.h (checked by tests/test_abi.py).
 EXPORTS = (
-    "hrs_create", "hrs_create_code", "hrs_code_kind", "hrs_destroy", "hrs_last_error", "hrs_version",
+    "hrs_create", "hrs_create_code", "hrs_create_src", "hrs_src_layout", "hrs_code_kind", "hrs_destroy",
+    "hrs_last_error", "hrs_version", "hrs_locations_to_read_list",
     "hrs_stripe_size", "hrs_parity_size", "hrs_symbol_size",
     "hrs_locations_to_read", "hrs_encode_matrix", "hrs_decode_matrix",
     "hrs_encode", "hrs_decode", "hrs_decode3",
@@ -68,6 +70,8 @@ def lib():
     sigs = {
         "hrs_create": ([I, I, ctypes.POINTER(HipOpts), ctypes.POINTER(P)], I),
         "hrs_create_code": ([I, I, I, ctypes.POINTER(HipOpts), ctypes.POINTER(P)], I),
+        "hrs_create_src": ([I, I, I, ctypes.POINTER(HipOpts), ctypes.POINTER(P)], I),
+        "hrs_src_layout": ([P, IP, IP, IP], I),
         "hrs_code_kind": ([P], I),
         "hrs_destroy": ([P], None),
         "hrs_last_error": ([P], ctypes.c_char_p),
@@ -76,6 +80,7 @@ def lib():
         "hrs_parity_size": ([P], I),
         "hrs_symbol_size": ([P], I),
         "hrs_locations_to_read": ([P, IP, I, IP], I),
+        "hrs_locations_to_read_list": ([P, IP, I, IP, IP], I),
         "hrs_encode_matrix": ([P, U8P], I),
         "hrs_decode_matrix": ([P, IP, I, IP, I, I, U8P], I),
         "hrs_encode": ([P, PP, PP, S], I),

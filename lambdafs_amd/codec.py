@@ -9,7 +9,7 @@ MI355X engine plugs in exactly there: set
 """
 import json
 
-from .erasure_code import HipNativeReedSolomonCode, HipReedSolomonCode, HipXORCode
+from .erasure_code import HipNativeReedSolomonCode, HipReedSolomonCode, HipSimpleRegeneratingCode, HipXORCode
 
 ERASURE_CODE_KEY_PREFIX = "hdfs.raid.erasure.code."  # Codec.java:52-53
 ERASURE_CODING_CODECS_KEY = "dfs.erasure_coding.codecs.json"  # DFSConfigKeys.java:558
@@ -34,6 +34,7 @@ ERASURE_CODE_CLASSES = {
     HipReedSolomonCode.JAVA_CLASS: HipReedSolomonCode,
     HipXORCode.JAVA_CLASS: HipXORCode,
     HipNativeReedSolomonCode.JAVA_CLASS: HipNativeReedSolomonCode,
+    HipSimpleRegeneratingCode.JAVA_CLASS: HipSimpleRegeneratingCode,
 }
 
 

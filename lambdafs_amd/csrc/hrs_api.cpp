@@ -21,6 +21,7 @@
 #include "crc32.hpp"
 #include "gf256.hpp"
 #include "hrs_crc.hpp"
+#include "hrs_host.hpp"
 #include "hrs_internal.hpp"
 
 using hrs::RowArgs;
@@ -34,9 +35,11 @@ struct hrs_codec {
   int device = 0;
   int kernel_mode = 0;
   std::vector<uint8_t> g;  // p x k
+  // SimpleRegeneratingCode: s SRC parities (after init's adjustment), r RS
+  // parities, group degree d, and each location's group neighbours
+  int src_s = 0, src_r = 0, src_d = 0;
+  std::vector<std::vector<int>> groups;
   hipStream_t stream = nullptr;
-  uint8_t* scratch = nullptr;  // device scratch for the host-buffer calls
-  size_t scratch_bytes = 0;
   std::map<std::vector<int>, std::vector<uint8_t>> decode_cache;
   // CRC-32 state (hrs_crc32_dev): fixed window tables, per-length fold tables, scratch
   uint32_t* crc_tables_a = nullptr;
@@ -54,6 +57,15 @@ struct hrs_codec {
     bool pending = false;
   } batch[2];
   int batch_next = 0;
+  // host-buffer calls: two chunk slots, each pinned staging + device rows +
+  // its own stream; a slot is reused once its D2H event has completed
+  struct HostSlot {
+    uint8_t* pin = nullptr;
+    uint8_t* dev = nullptr;
+    size_t bytes = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+  } host[2];
   std::string err;
 };
 
@@ -136,28 +148,21 @@ bool gf_invert(std::vector<uint8_t>& a, int m) {
   return true;
 }
 
-// Decode matrix in closed form (see hrs.h). With x_j = alpha^ntr[j] and
-// syndromes S_i = sum_l A[i][l] d_l, A[i][l] = alpha^(i*l) (0 where zeroed),
-// the reference solves V z = S with V[i][j] = x_j^i
-// (GaloisField.java:232-246; ReedSolomonCode.java:127-142), so z = V^-1 A d.
-hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
-                               int zero_ntr, std::vector<uint8_t>& d) {
-  const int n = c->n;
+// Decode rows in closed form over an RS stripe of n locations (see hrs.h).
+// With x_j = alpha^ntr[j] and syndromes S_i = sum_l A[i][l] d_l,
+// A[i][l] = alpha^(i*l) (0 where zeroed), the reference solves V z = S with
+// V[i][j] = x_j^i (GaloisField.java:232-246; ReedSolomonCode.java:127-142),
+// so z = V^-1 A d. Locations are validated by the caller.
+bool rs_decode_rows(int n, const int* erased, int ne, const int* ntr, int nn, int zero_ntr, std::vector<uint8_t>& d) {
   d.assign(static_cast<size_t>(ne) * n, 0);
-  if (ne == 0 || nn == 0) return HRS_OK;
+  if (ne == 0 || nn == 0) return true;
   std::vector<char> in_ntr(n, 0);
-  for (int j = 0; j < nn; ++j) {
-    if (ntr[j] < 0 || ntr[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range [0,%d)", ntr[j], n);
-    if (in_ntr[ntr[j]]) return fail(c, HRS_EINVAL, "duplicate location %d", ntr[j]);
-    in_ntr[ntr[j]] = 1;
-  }
-  for (int t = 0; t < ne; ++t)
-    if (erased[t] < 0 || erased[t] >= n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  for (int j = 0; j < nn; ++j) in_ntr[ntr[j]] = 1;
   const int m = nn;
   std::vector<uint8_t> v(static_cast<size_t>(m) * m);
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < m; ++j) v[i * m + j] = gf::alpha_pow(static_cast<long>(ntr[j]) * i);
-  if (!gf_invert(v, m)) return fail(c, HRS_EINVAL, "singular Vandermonde system");
+  if (!gf_invert(v, m)) return false;
   for (int t = 0; t < ne; ++t) {
     int j = -1;
     for (int q = 0; q < nn; ++q)
@@ -173,6 +178,21 @@ hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const in
       d[static_cast<size_t>(t) * n + l] = acc;
     }
   }
+  return true;
+}
+
+hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
+                               int zero_ntr, std::vector<uint8_t>& d) {
+  const int n = c->n;
+  std::vector<char> in_ntr(n, 0);
+  for (int j = 0; j < nn; ++j) {
+    if (ntr[j] < 0 || ntr[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range [0,%d)", ntr[j], n);
+    if (in_ntr[ntr[j]]) return fail(c, HRS_EINVAL, "duplicate location %d", ntr[j]);
+    in_ntr[ntr[j]] = 1;
+  }
+  for (int t = 0; t < ne; ++t)
+    if (erased[t] < 0 || erased[t] >= n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  if (!rs_decode_rows(n, erased, ne, ntr, nn, zero_ntr, d)) return fail(c, HRS_EINVAL, "singular Vandermonde system");
   return HRS_OK;
 }
 
@@ -253,6 +273,160 @@ hrs_status build_nrs_decode_matrix(hrs_codec* c, int ne, const int* ntr, int nn,
   return HRS_OK;
 }
 
+// ------------------------------------------------ SimpleRegeneratingCode
+// (SimpleRegeneratingCode.java). Locations: [SRC parities 0..s-1, RS
+// parities s..p-1, data p..n-1]; the RS stripe is locations s..n-1 (RS
+// parities first). Group g < s = SRC parity g + RS-stripe positions
+// [g*d, (g+1)*d); the last ("implied") group = the remaining RS-stripe
+// positions + every SRC parity.
+
+int src_group(const hrs_codec* c, int loc) {  // getSRCGroup, :415-426
+  if (0 <= loc && loc < c->src_s) return loc;
+  if (c->src_s <= loc && loc < c->n) return (loc - c->src_s) / c->src_d;
+  return -1;
+}
+
+std::vector<int> src_neighbors(const hrs_codec* c, int loc) {  // getSRCGroupNeighbors, :371-409
+  std::vector<int> v;
+  const int g = src_group(c, loc), s = c->src_s, d = c->src_d;
+  if (g < s) {
+    if (g != loc) v.push_back(g);
+    for (int i = s + g * d; i < s + (g + 1) * d; ++i)
+      if (i != loc) v.push_back(i);
+  } else {
+    for (int i = 0; i < s; ++i) v.push_back(i);
+    for (int i = s + g * d; i < c->n; ++i)
+      if (i != loc) v.push_back(i);
+  }
+  return v;
+}
+
+// init's adjustment (:70-90): fewer SRC parities until the groups fit
+void src_params(int k, int p, int s_in, int* s, int* r, int* d) {
+  int ss = s_in, rr = p - s_in;
+  int dd = (k + rr + ss) / (ss + 1);  // ceil((k + r) / (s + 1))
+  while (dd * ss >= k + rr) {
+    --ss;
+    ++rr;
+    dd = (k + rr + ss) / (ss + 1);
+  }
+  *s = ss;
+  *r = rr;
+  *d = dd;
+}
+
+bool src_conflict(const hrs_codec* c, const int* locs, int n) {  // groupConflict, :432-453
+  std::vector<int> count(c->src_s + 1, 0);
+  for (int i = 0; i < n; ++i)
+    if (locs[i] < c->src_s) {
+      count[c->src_s] = 1;
+      break;
+    }
+  for (int i = 0; i < n; ++i)
+    if (count[src_group(c, locs[i])]++ > 0) return true;
+  return false;
+}
+
+// locationsToReadForDecode, :300-366 (an ordered list of variable length)
+hrs_status src_locations(hrs_codec* c, const int* erased, int ne, std::vector<int>& out) {
+  out.clear();
+  for (int i = 0; i < ne; ++i)
+    if (erased[i] < 0 || erased[i] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[i]);
+  if (ne == 1) {
+    out = c->groups[erased[0]];
+    return HRS_OK;
+  }
+  if (!src_conflict(c, erased, ne)) {
+    for (int i = 0; i < ne; ++i)
+      for (int loc : c->groups[erased[i]])
+        if (std::find(out.begin(), out.end(), loc) == out.end()) out.push_back(loc);
+    return HRS_OK;
+  }
+  for (int loc = c->src_s; loc < c->n && static_cast<int>(out.size()) < c->k; ++loc)
+    if (std::find(erased, erased + ne, loc) == erased + ne) out.push_back(loc);
+  if (static_cast<int>(out.size()) != c->k) {
+    std::string s = "Locations ";
+    for (int i = 0; i < ne; ++i) s += " " + std::to_string(erased[i]);
+    return fail(c, HRS_ETOOMANY, "%s", s.c_str());
+  }
+  return HRS_OK;
+}
+
+// p x k: RS parities = the hops generator over r roots (same construction as
+// ReedSolomonCode); SRC parity i = XOR of RS-stripe positions [d*i, d*(i+1))
+// (encode, :116-157).
+void src_encode_matrix(hrs_codec* c) {
+  const int k = c->k, s = c->src_s, r = c->src_r, d = c->src_d;
+  std::vector<uint8_t> grs(static_cast<size_t>(r) * k);
+  gf::encode_matrix(k, r, grs.data());
+  std::fill(c->g.begin(), c->g.end(), 0);
+  for (int i = 0; i < r; ++i)
+    for (int j = 0; j < k; ++j) c->g[static_cast<size_t>(s + i) * k + j] = grs[static_cast<size_t>(i) * k + j];
+  for (int i = 0; i < s; ++i)
+    for (int j = d * i; j < d * (i + 1); ++j) {
+      if (j < r)
+        for (int q = 0; q < k; ++q) c->g[static_cast<size_t>(i) * k + q] ^= grs[static_cast<size_t>(j) * k + q];
+      else
+        c->g[static_cast<size_t>(i) * k + (j - r)] ^= 1;
+    }
+}
+
+// decode 5-arg, :194-277, as an ne x n matrix over the read values:
+//  one erasure      -> XOR of locationsToRead;
+//  no group clash   -> XOR of each erased location's group;
+//  otherwise        -> RS decode of the RS stripe at its not-to-read
+//                      positions (decodeReedSolomon, :162-182), then each
+//                      erased SRC parity = XOR of its (repaired) group.
+hrs_status build_src_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* to_read, int nr, const int* ntr,
+                                   int nn, std::vector<uint8_t>& d) {
+  const int n = c->n, s = c->src_s, r = c->src_r, nrs = c->n - c->src_s;
+  for (int t = 0; t < ne; ++t)
+    if (erased[t] < 0 || erased[t] >= n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  for (int j = 0; j < nr; ++j)
+    if (to_read[j] < 0 || to_read[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range", to_read[j]);
+  for (int j = 0; j < nn; ++j)
+    if (ntr[j] < 0 || ntr[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range", ntr[j]);
+  d.assign(static_cast<size_t>(ne) * n, 0);
+  if (ne == 1) {
+    for (int j = 0; j < nr; ++j) d[to_read[j]] ^= 1;
+    return HRS_OK;
+  }
+  if (!src_conflict(c, erased, ne)) {
+    for (int t = 0; t < ne; ++t)
+      for (int loc : c->groups[erased[t]]) d[static_cast<size_t>(t) * n + loc] ^= 1;
+    return HRS_OK;
+  }
+  std::vector<int> ers;
+  for (int j = 0; j < nn; ++j)
+    if (ntr[j] >= s) ers.push_back(ntr[j] - s);
+  const int m = static_cast<int>(ers.size());
+  if (m > r) return fail(c, HRS_EINVAL, "%d not-to-read RS locations > %d RS parities", m, r);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < i; ++j)
+      if (ers[i] == ers[j]) return fail(c, HRS_EINVAL, "duplicate location %d", ers[i] + s);
+  std::vector<uint8_t> drs;
+  if (!rs_decode_rows(nrs, ers.data(), m, ers.data(), m, 1, drs)) return fail(c, HRS_EINVAL, "singular Vandermonde system");
+  // row of location l after the RS repair, over the read values
+  auto fixed = [&](int l, uint8_t* row) {
+    if (l >= s) {
+      for (int q = 0; q < m; ++q)
+        if (ers[q] == l - s) {
+          for (int col = 0; col < nrs; ++col) row[s + col] ^= drs[static_cast<size_t>(q) * nrs + col];
+          return;
+        }
+    }
+    row[l] ^= 1;
+  };
+  for (int t = 0; t < ne; ++t) {
+    uint8_t* row = &d[static_cast<size_t>(t) * n];
+    if (erased[t] < s)
+      for (int loc : c->groups[erased[t]]) fixed(loc, row);
+    else
+      fixed(erased[t], row);
+  }
+  return HRS_OK;
+}
+
 // ---------------------------------------------------------------- dispatch
 
 // The matrix a 5-arg decodeBulk applies (ne x n), per code family.
@@ -263,7 +437,8 @@ hrs_status build_nrs_decode_matrix(hrs_codec* c, int ne, const int* ntr, int nn,
 //       (XORCode.java:115-145 ignores toRead/notToRead). Rows the caller passes
 //       as NULL are the zeros the reference reads there (StripeReader.java:111-120).
 hrs_status decode5_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
-                          const uint8_t* const* rows, std::vector<uint8_t>& tmp, const uint8_t** out) {
+                          const uint8_t* const* rows, std::vector<uint8_t>& tmp, const uint8_t** out,
+                          const int* to_read = nullptr, int nr = -1) {
   for (int t = 0; t < ne; ++t)
     if (erased[t] < 0 || erased[t] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
   if (c->kind == HRS_CODE_XOR) {
@@ -274,6 +449,33 @@ hrs_status decode5_matrix(hrs_codec* c, const int* erased, int ne, const int* nt
       for (int l = 0; l < c->n; ++l)
         if (!rows[l]) tmp[l] = 0;
     *out = tmp.data();
+    return HRS_OK;
+  }
+  if (c->kind == HRS_CODE_SRC) {
+    // without an explicit locationsToRead (device calls), it is every
+    // location outside not_to_read, as Decoder.java:303-338 builds them
+    std::vector<int> tr;
+    if (!to_read || nr < 0) {
+      for (int l = 0; l < c->n; ++l)
+        if (std::find(ntr, ntr + nn, l) == ntr + nn) tr.push_back(l);
+    } else {
+      tr.assign(to_read, to_read + nr);
+    }
+    std::vector<int> key{3, ne};
+    key.insert(key.end(), erased, erased + ne);
+    key.push_back(static_cast<int>(tr.size()));
+    key.insert(key.end(), tr.begin(), tr.end());
+    key.push_back(nn);
+    key.insert(key.end(), ntr, ntr + nn);
+    auto it = c->decode_cache.find(key);
+    if (it == c->decode_cache.end()) {
+      std::vector<uint8_t> d;
+      hrs_status st = build_src_decode_matrix(c, erased, ne, tr.data(), static_cast<int>(tr.size()), ntr, nn, d);
+      if (st != HRS_OK) return st;
+      if (c->decode_cache.size() > 4096) c->decode_cache.clear();
+      it = c->decode_cache.emplace(key, std::move(d)).first;
+    }
+    *out = it->second.data();
     return HRS_OK;
   }
   if (c->kind == HRS_CODE_RS && nn > c->p)
@@ -431,55 +633,118 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
 }
 
 // Device scratch for the host-buffer calls: `rows` rows of `pitch` bytes.
-hrs_status ensure_scratch(hrs_codec* c, size_t bytes) {
-  if (c->scratch_bytes >= bytes) return HRS_OK;
-  if (c->scratch) {
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->scratch);
-    c->scratch = nullptr;
-    c->scratch_bytes = 0;
+size_t pitch_for(size_t len) { return (len + 255) & ~static_cast<size_t>(255); }
+
+// Host rows -> device, apply m, device -> host rows; synchronous. The rows
+// (pageable: a JNI-pinned Java array) go through pinned staging in column
+// chunks over two slots: while the copy pool moves chunk j into one slot's
+// staging (and chunk j-2's outputs out of it), the GPU runs chunk j-1's H2D,
+// kernel and D2H on the other slot's stream.
+size_t host_chunk_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("HRS_HOST_CHUNK");
+    long x = e ? atol(e) : 0;
+    if (x < static_cast<long>(hrs::kWindowBytes)) x = 512 << 10;  // measured best (tools/host_sweep.sh)
+    return static_cast<size_t>(x) / hrs::kWindowBytes * hrs::kWindowBytes;
+  }();
+  return v;
+}
+
+hrs_status host_slot(hrs_codec* c, int i, size_t bytes) {
+  hrs_codec::HostSlot& h = c->host[i];
+  if (!h.stream) {
+    hipError_t e = hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(c, e, "hipStreamCreate");
+    e = hipEventCreateWithFlags(&h.done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
   }
-  hipError_t e = hipMalloc(&c->scratch, bytes);
+  if (h.bytes >= bytes) return HRS_OK;
+  (void)hipStreamSynchronize(h.stream);
+  if (h.dev) (void)hipFree(h.dev);
+  if (h.pin) (void)hipHostFree(h.pin);
+  h.dev = nullptr;
+  h.pin = nullptr;
+  h.bytes = 0;
+  hipError_t e = hipMalloc(&h.dev, bytes);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
-  c->scratch_bytes = bytes;
+  e = hipHostMalloc(&h.pin, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  h.bytes = bytes;
   return HRS_OK;
 }
 
-size_t pitch_for(size_t len) { return (len + 255) & ~static_cast<size_t>(255); }
-
-// Host rows -> device, apply m, device -> host rows; synchronous.
 hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                       uint8_t* const* out_rows, size_t len, bool static_kp) {
   if (len == 0 || nout == 0) return HRS_OK;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
-  const size_t pitch = pitch_for(len);
-  hrs_status st = ensure_scratch(c, pitch * (nin + nout));
-  if (st != HRS_OK) return st;
-  std::vector<const uint8_t*> din(nin, nullptr);
-  std::vector<uint8_t*> dout(nout);
+  std::vector<int> slot_of(nin, -1);  // staging row of each live input
+  int nlive = 0;
   for (int i = 0; i < nin; ++i) {
     bool any = false;
     for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
     if (!any) continue;
     if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
-    uint8_t* d = c->scratch + pitch * i;
-    hipError_t e = hipMemcpyAsync(d, in_rows[i], len, hipMemcpyHostToDevice, c->stream);
-    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
-    din[i] = d;
+    slot_of[i] = nlive++;
   }
-  for (int o = 0; o < nout; ++o) {
+  for (int o = 0; o < nout; ++o)
     if (!out_rows[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
-    dout[o] = c->scratch + pitch * (nin + o);
+  const size_t chunk = std::min(len, host_chunk_bytes());
+  const size_t pitch = pitch_for(chunk);
+  const size_t nchunks = (len + chunk - 1) / chunk;
+  const size_t need = pitch * static_cast<size_t>(nlive + nout);
+  for (int i = 0; i < 2; ++i) {
+    hrs_status st = host_slot(c, i, need);
+    if (st != HRS_OK) return st;
   }
-  st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, c->stream, static_kp);
-  if (st != HRS_OK) return st;
-  for (int o = 0; o < nout; ++o) {
-    hipError_t e = hipMemcpyAsync(out_rows[o], dout[o], len, hipMemcpyDeviceToHost, c->stream);
+  hrs::CopyPool& pool = hrs::CopyPool::instance();
+  std::vector<hrs::CopyJob> jobs;
+  size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
+  bool pending[2] = {false, false};
+  auto finish = [&](int sl) -> hrs_status {  // wait for a slot, copy its outputs out
+    if (!pending[sl]) return HRS_OK;
+    hipError_t e = hipEventSynchronize(c->host[sl].done);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
+    jobs.clear();
+    for (int o = 0; o < nout; ++o)
+      jobs.push_back({out_rows[o] + pend_off[sl], c->host[sl].pin + pitch * (nlive + o), pend_len[sl]});
+    pool.run(jobs);
+    pending[sl] = false;
+    return HRS_OK;
+  };
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  for (size_t j = 0; j < nchunks; ++j) {
+    const int sl = static_cast<int>(j & 1);
+    hrs_codec::HostSlot& h = c->host[sl];
+    hrs_status st = finish(sl);
+    if (st != HRS_OK) return st;
+    const size_t off = j * chunk, lj = std::min(chunk, len - off);
+    jobs.clear();
+    for (int i = 0; i < nin; ++i)
+      if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
+    pool.run(jobs);
+    if (nlive > 0) {
+      hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
+    }
+    for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? h.dev + pitch * slot_of[i] : nullptr;
+    for (int o = 0; o < nout; ++o) dout[o] = h.dev + pitch * (nlive + o);
+    st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
+    if (st != HRS_OK) return st;
+    hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, pitch * (nout - 1) + lj,
+                                  hipMemcpyDeviceToHost, h.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+    e = hipEventRecord(h.done, h.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+    pending[sl] = true;
+    pend_off[sl] = off;
+    pend_len[sl] = lj;
   }
-  hipError_t e = hipStreamSynchronize(c->stream);
-  if (e != hipSuccess) return hip_fail(c, e, "hipStreamSynchronize");
+  for (size_t j = nchunks > 2 ? nchunks - 2 : 0; j < nchunks; ++j) {
+    hrs_status st = finish(static_cast<int>(j & 1));
+    if (st != HRS_OK) return st;
+  }
   return HRS_OK;
 }
 
@@ -487,6 +752,8 @@ void init_encode_matrix(hrs_codec* c) {
   c->g.resize(static_cast<size_t>(c->p) * c->k);
   if (c->kind == HRS_CODE_XOR) {
     std::fill(c->g.begin(), c->g.end(), 1);  // XORCode.encodeBulk, XORCode.java:99-113
+  } else if (c->kind == HRS_CODE_SRC) {
+    src_encode_matrix(c);
   } else if (c->kind == HRS_CODE_NRS) {
     // Cauchy rows of ISA-L gf_gen_cauchy1_matrix (erasure_coder.c:47-60):
     // parity r = Apache row k + r, G[r][c] = 1 / ((k + r) ^ c)
@@ -630,10 +897,30 @@ hrs_status hrs_create(int stripe_size, int parity_size, const hrs_opts* opts, hr
 
 int hrs_code_kind(const hrs_codec* c) { return c ? c->kind : -1; }
 
-hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out) {
+}  // extern "C"
+
+namespace {
+
+void init_code(hrs_codec* c, int code, int k, int p, int src_s) {
+  c->k = k;
+  c->p = p;
+  c->n = k + p;
+  c->kind = code;
+  if (code == HRS_CODE_SRC) {
+    src_params(k, p, src_s, &c->src_s, &c->src_r, &c->src_d);
+    c->groups.resize(c->n);
+    for (int l = 0; l < c->n; ++l) c->groups[l] = src_neighbors(c, l);
+  }
+  init_encode_matrix(c);
+}
+
+hrs_status create_impl(int code, int stripe_size, int parity_size, int src_s, const hrs_opts* opts, hrs_codec** out) {
   if (!out) return fail(nullptr, HRS_EINVAL, "out is NULL");
   *out = nullptr;
-  if (code != HRS_CODE_RS && code != HRS_CODE_XOR && code != HRS_CODE_NRS) return fail(nullptr, HRS_EINVAL, "unknown code family %d", code);
+  if (code != HRS_CODE_RS && code != HRS_CODE_XOR && code != HRS_CODE_NRS && code != HRS_CODE_SRC)
+    return fail(nullptr, HRS_EINVAL, "unknown code family %d", code);
+  if (code == HRS_CODE_SRC && (src_s < 0 || src_s > parity_size))
+    return fail(nullptr, HRS_EINVAL, "SRC parities %d outside [0, parity size %d]", src_s, parity_size);
   if (code == HRS_CODE_XOR && parity_size != 1)
     return fail(nullptr, HRS_EINVAL, "XOR code needs parity size 1 (XORCode.java:47), got %d", parity_size);
   if (stripe_size < 1 || parity_size < 1 || stripe_size + parity_size >= gf::kFieldSize ||
@@ -646,12 +933,8 @@ hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs
   int dev = opts ? opts->device : -1;
   if (dev == HRS_DEVICE_NONE) {  // host-only handle: matrices and locations, no coding
     auto* c = new hrs_codec();
-    c->k = stripe_size;
-    c->p = parity_size;
-    c->n = stripe_size + parity_size;
     c->device = HRS_DEVICE_NONE;
-    c->kind = code;
-    init_encode_matrix(c);
+    init_code(c, code, stripe_size, parity_size, src_s);
     *out = c;
     return HRS_OK;
   }
@@ -664,12 +947,8 @@ hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs
   if (e != hipSuccess || dev >= ndev)
     return fail(nullptr, HRS_EDEVICE, "no HIP device %d (%s)", dev, hipGetErrorString(e));
   auto* c = new hrs_codec();
-  c->k = stripe_size;
-  c->p = parity_size;
-  c->n = stripe_size + parity_size;
   c->device = dev;
-  c->kind = code;
-  init_encode_matrix(c);
+  init_code(c, code, stripe_size, parity_size, src_s);
   {
     DeviceGuard g(dev);
     e = g.ok ? hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) : hipErrorInvalidDevice;
@@ -679,6 +958,29 @@ hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs
     return fail(nullptr, HRS_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
   }
   *out = c;
+  return HRS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+hrs_status hrs_create_code(int code, int stripe_size, int parity_size, const hrs_opts* opts, hrs_codec** out) {
+  // HRS_CODE_SRC here = the Java's deprecated (stripeSize, paritySize)
+  // constructor: no SRC parities (SimpleRegeneratingCode.java:44-47)
+  return create_impl(code, stripe_size, parity_size, 0, opts, out);
+}
+
+hrs_status hrs_create_src(int stripe_size, int parity_size, int src_parity_size, const hrs_opts* opts,
+                          hrs_codec** out) {
+  return create_impl(HRS_CODE_SRC, stripe_size, parity_size, src_parity_size, opts, out);
+}
+
+hrs_status hrs_src_layout(const hrs_codec* c, int* src_parities, int* rs_parities, int* group_degree) {
+  if (!c || c->kind != HRS_CODE_SRC) return HRS_EINVAL;
+  if (src_parities) *src_parities = c->src_s;
+  if (rs_parities) *rs_parities = c->src_r;
+  if (group_degree) *group_degree = c->src_d;
   return HRS_OK;
 }
 
@@ -693,10 +995,18 @@ void hrs_destroy(hrs_codec* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
   }
-  if (c->scratch) (void)hipFree(c->scratch);
   if (c->crc_tables_a) (void)hipFree(c->crc_tables_a);
   for (auto& kv : c->crc_fold_tables) (void)hipFree(kv.second);
   if (c->crc_raw) (void)hipFree(c->crc_raw);
+  for (auto& h : c->host) {
+    if (h.stream) {
+      (void)hipStreamSynchronize(h.stream);
+      (void)hipStreamDestroy(h.stream);
+    }
+    if (h.done) (void)hipEventDestroy(h.done);
+    if (h.dev) (void)hipFree(h.dev);
+    if (h.pin) (void)hipHostFree(h.pin);
+  }
   for (auto& b : c->batch) {
     if (b.done) {
       (void)hipEventSynchronize(b.done);
@@ -720,9 +1030,19 @@ hrs_status hrs_set_kernel_mode(hrs_codec* c, int mode) {
   return HRS_OK;
 }
 
-hrs_status hrs_locations_to_read(const hrs_codec* cc, const int* erased, int num_erased, int* to_read) {
+hrs_status hrs_locations_to_read_list(const hrs_codec* cc, const int* erased, int num_erased, int* to_read,
+                                      int* num_to_read) {
   auto* c = const_cast<hrs_codec*>(cc);
-  if (!c || !to_read || num_erased < 0 || (num_erased > 0 && !erased)) return HRS_EINVAL;
+  if (!c || !to_read || !num_to_read || num_erased < 0 || (num_erased > 0 && !erased)) return HRS_EINVAL;
+  *num_to_read = 0;
+  if (c->kind == HRS_CODE_SRC) {
+    std::vector<int> v;
+    hrs_status st = src_locations(c, erased, num_erased, v);
+    if (st != HRS_OK) return st;
+    std::copy(v.begin(), v.end(), to_read);
+    *num_to_read = static_cast<int>(v.size());
+    return HRS_OK;
+  }
   // ErasureCode.java:89-113: scan locations from the top, keep the first k good ones.
   int got = 0;
   for (int loc = c->n - 1; loc >= 0 && got < c->k; --loc) {
@@ -735,6 +1055,20 @@ hrs_status hrs_locations_to_read(const hrs_codec* cc, const int* erased, int num
     for (int i = 0; i < num_erased; ++i) s += " " + std::to_string(erased[i]);
     return fail(c, HRS_ETOOMANY, "%s", s.c_str());
   }
+  *num_to_read = got;
+  return HRS_OK;
+}
+
+hrs_status hrs_locations_to_read(const hrs_codec* cc, const int* erased, int num_erased, int* to_read) {
+  auto* c = const_cast<hrs_codec*>(cc);
+  if (!c || !to_read || num_erased < 0 || (num_erased > 0 && !erased)) return HRS_EINVAL;
+  std::vector<int> v(c->n);
+  int m = 0;
+  hrs_status st = hrs_locations_to_read_list(c, erased, num_erased, v.data(), &m);
+  if (st != HRS_OK) return st;
+  if (m != c->k)
+    return fail(c, HRS_EINVAL, "%d locations to read (not stripe_size): use hrs_locations_to_read_list", m);
+  std::copy(v.begin(), v.begin() + m, to_read);
   return HRS_OK;
 }
 
@@ -753,6 +1087,10 @@ hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, con
   if (c->kind == HRS_CODE_XOR) {
     const uint8_t* x = nullptr;
     st = decode5_matrix(c, erased, ne, ntr, nn, nullptr, m, &x);
+  } else if (c->kind == HRS_CODE_SRC) {
+    const uint8_t* x = nullptr;
+    st = decode5_matrix(c, erased, ne, ntr, nn, nullptr, m, &x);
+    if (st == HRS_OK && ne > 0) m.assign(x, x + static_cast<size_t>(ne) * c->n);
   } else if (c->kind == HRS_CODE_NRS) {
     for (int t = 0; t < ne; ++t)
       if (erased[t] < 0 || erased[t] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
@@ -781,7 +1119,7 @@ hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* co
   if (ne == 0 && c->kind == HRS_CODE_RS) return HRS_OK;
   std::vector<uint8_t> tmp;
   const uint8_t* d = nullptr;
-  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d);
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d, to_read, to_read ? nr : -1);
   if (st != HRS_OK) return st;
   return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
 }
@@ -797,8 +1135,8 @@ hrs_status hrs_decode3(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* c
     if (st != HRS_OK) return st;
     return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
   }
-  if (c->kind == HRS_CODE_NRS)  // NativeReedSolomonCode has no 3-arg decodeBulk
-    return fail(c, HRS_EINVAL, "decodeBulk(readBufs, writeBufs, erasedLocations) is not supported by nrs");
+  if (c->kind == HRS_CODE_NRS || c->kind == HRS_CODE_SRC)  // only ReedSolomonCode / XORCode have it
+    return fail(c, HRS_EINVAL, "decodeBulk(readBufs, writeBufs, erasedLocations) is not supported by this code");
   if (ne == 0) return HRS_OK;  // ReedSolomonCode.java:170-172
   if (ne > c->p) return fail(c, HRS_EINVAL, "%d erasures > parity size %d", ne, c->p);  // errSignature[p]
   hrs_status st;
@@ -849,7 +1187,7 @@ hrs_status hrs_decode_batch_dev(hrs_codec* c, const uint8_t* stripes, size_t row
   std::vector<std::vector<uint8_t>> mats;  // per pattern: ne x n decode matrix
   bool fused = true;
   int max_nout = 0, max_nin = 0;
-  std::vector<int> key, to_read(c->k), ntr;
+  std::vector<int> key, to_read(c->n), ntr;
   for (size_t s = 0; s < nstripes; ++s) {
     key.clear();
     for (int t = 0; t < max_erased && erased[s * max_erased + t] >= 0; ++t) key.push_back(erased[s * max_erased + t]);
@@ -864,14 +1202,20 @@ hrs_status hrs_decode_batch_dev(hrs_codec* c, const uint8_t* stripes, size_t row
     hrs::BatchPlan pl{};
     std::vector<uint8_t> m(static_cast<size_t>(ne) * c->n, 0);
     if (ne > 0) {
-      hrs_status st = hrs_locations_to_read(c, key.data(), ne, to_read.data());
+      int nr = 0;
+      hrs_status st = hrs_locations_to_read_list(c, key.data(), ne, to_read.data(), &nr);
       if (st != HRS_OK) return st;
-      ntr.clear();
+      ntr.clear();  // Decoder.java:303-338: everything not read, erased included
       for (int l = 0; l < c->n; ++l)
-        if (std::find(to_read.begin(), to_read.end(), l) == to_read.end()) ntr.push_back(l);
+        if (std::find(to_read.begin(), to_read.begin() + nr, l) == to_read.begin() + nr ||
+            std::find(key.begin(), key.end(), l) != key.end())
+          ntr.push_back(l);
+      std::vector<int> tr_sorted(to_read.begin(), to_read.begin() + nr);
+      std::sort(tr_sorted.begin(), tr_sorted.end());
       std::vector<uint8_t> tmp;
       const uint8_t* d = nullptr;
-      st = decode5_matrix(c, key.data(), ne, ntr.data(), static_cast<int>(ntr.size()), nullptr, tmp, &d);
+      st = decode5_matrix(c, key.data(), ne, ntr.data(), static_cast<int>(ntr.size()), nullptr, tmp, &d,
+                          tr_sorted.data(), nr);
       if (st != HRS_OK) return st;
       std::memcpy(m.data(), d, m.size());
       for (int l = 0; l < c->n; ++l) {

@@ -199,6 +199,17 @@ class _HipErasureCode(ErasureCode):
     def symbolSize(self):
         return _lib.lib().hrs_symbol_size(self._handle())
 
+    def locationsToReadForDecode(self, erasedLocations):
+        """The product's locationsToReadForDecode (hrs_locations_to_read_list):
+        ErasureCode.java:89-113, or SimpleRegeneratingCode.java:300-366."""
+        n = self._k + self._p
+        buf = (ctypes.c_int * max(1, n))()
+        cnt = ctypes.c_int(0)
+        erased = [int(e) for e in erasedLocations]
+        self._check(_lib.lib().hrs_locations_to_read_list(self._handle(), int_array(erased), len(erased), buf,
+                                                           ctypes.byref(cnt)))
+        return list(buf[: cnt.value])
+
     def setKernelMode(self, mode):
         """0 auto, 1 runtime-matrix bit-sliced kernel, 2 byte-granular kernel."""
         self._check(_lib.lib().hrs_set_kernel_mode(self._handle(), int(mode)))
@@ -409,6 +420,80 @@ class HipNativeReedSolomonCode(_HipErasureCode):
         if len(writeBufs) > len(locationsNotToRead):
             # bwriteBufs holds |locationsNotToRead| buffers (NativeReedSolomonCode.java:96, :145-149)
             raise IndexError("more write buffers than not-to-read locations")
+        super().decodeBulk(readBufs, writeBufs, erasedLocations, locationsToRead, locationsNotToRead)
+
+
+class HipSimpleRegeneratingCode(_HipErasureCode):
+    """Drop-in for SimpleRegeneratingCode (the `src` codec,
+    hops-erasure-coding/.../SimpleRegeneratingCode.java:28-482): RS(k, r)
+    plus s stored local XOR parities ("parity_length_src" in the codec JSON;
+    init's adjustment loop may lower it, see srcLayout()). Bulk calls follow
+    ErasureCode's default per-column loops (ErasureCode.java:136-181) over the
+    Java's scalar encode/decode, computed here as matrices on the GPU.
+
+    Not mirrored: the 3-argument scalar decode (an RS decode over the whole
+    stripe, SimpleRegeneratingCode.java:188-191, which indexes past its tables
+    for locations >= k + r) and the scalar decode's side effects on `data`
+    (ErasureCode.decodeBulk hands it a scratch copy, so bulk callers never see
+    them)."""
+
+    CODE_KIND = _lib.HRS_CODE_SRC
+    JAVA_CLASS = "io.hops.erasure_coding.HipSimpleRegeneratingCode"
+
+    def __init__(self, stripeSize=None, paritySize=None, paritySizeSRC=0, device=None):
+        self._src_in = int(paritySizeSRC)
+        super().__init__(stripeSize, paritySize, device)
+
+    def init(self, codec):
+        """SimpleRegeneratingCode.init(Codec), :52-64."""
+        self._src_in = int(codec.json.get("parity_length_src", 0))
+        self._init(codec.stripeLength, codec.parityLength)
+
+    def _init(self, k, p):
+        L = _lib.lib()
+        self.close()
+        opts = _lib.HipOpts()
+        opts.device = -1 if self._device is None else int(self._device)
+        h = ctypes.c_void_p()
+        check(L.hrs_create_src(int(k), int(p), self._src_in, ctypes.byref(opts), ctypes.byref(h)))
+        self._h = h
+        self._k, self._p = int(k), int(p)
+
+    def srcLayout(self):
+        """(stored SRC parities s, RS parities r, group degree d) after init."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(_lib.lib().hrs_src_layout(self._handle(), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def encode(self, message, parity):
+        """SimpleRegeneratingCode.encode, :116-157."""
+        if len(message) != self._k or len(parity) != self._p:
+            raise ValueError("message/parity length mismatch")
+        ins = [np.array([_symbol(v)], dtype=np.uint8) for v in message]
+        outs = [np.zeros(1, dtype=np.uint8) for _ in range(self._p)]
+        self.encodeBulk(ins, outs)
+        for i in range(self._p):
+            parity[i] = int(outs[i][0])
+
+    def decode(self, data, erasedLocations, erasedValues, locationsToRead=None, locationsNotToRead=None):
+        """5-arg SimpleRegeneratingCode.decode, :194-277."""
+        if locationsNotToRead is None:
+            raise NotImplementedError("3-argument SimpleRegeneratingCode.decode is not provided")
+        n = self._k + self._p
+        if len(data) != n or len(erasedValues) != len(erasedLocations):
+            raise ValueError("data/erasedValues length mismatch")
+        if not erasedLocations:
+            return
+        rows = [np.array([_symbol(v)], dtype=np.uint8) for v in data]
+        outs = [np.zeros(1, dtype=np.uint8) for _ in erasedLocations]
+        self.decodeBulk(rows, outs, list(erasedLocations), list(locationsToRead or []), list(locationsNotToRead))
+        for i in range(len(erasedLocations)):
+            erasedValues[i] = int(outs[i][0])
+
+    def decodeBulk(self, readBufs, writeBufs, erasedLocations, locationsToRead=None, locationsNotToRead=None):
+        """ErasureCode.decodeBulk (ErasureCode.java:162-181) over the 5-arg decode."""
+        if locationsNotToRead is None:
+            raise NotImplementedError("SimpleRegeneratingCode has no 3-argument decodeBulk")
         super().decodeBulk(readBufs, writeBufs, erasedLocations, locationsToRead, locationsNotToRead)
 
 

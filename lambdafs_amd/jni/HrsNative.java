@@ -11,6 +11,7 @@ final class HrsNative {
   static final int CODE_RS = 0;   // HRS_CODE_RS
   static final int CODE_XOR = 1;  // HRS_CODE_XOR
   static final int CODE_NRS = 2;  // HRS_CODE_NRS
+  static final int CODE_SRC = 3;  // HRS_CODE_SRC
 
   static {
     System.loadLibrary("hrs_jni");  // libhrs_jni.so -> libhrs.so
@@ -21,7 +22,12 @@ final class HrsNative {
 
   static native long create(int code, int stripeSize, int paritySize);
 
+  static native long createSrc(int stripeSize, int paritySize, int srcParitySize);
+
   static native void destroy(long codec);
+
+  // hrs_locations_to_read_list; throws TooManyErasedLocations
+  static native int[] locationsToRead(long codec, int[] erased) throws TooManyErasedLocations;
 
   static native void encode(long codec, byte[][] inputs, byte[][] outputs, int len) throws IOException;
 

@@ -68,6 +68,37 @@ JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv* en
   return (jlong)(intptr_t)c;
 }
 
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_createSrc(JNIEnv* env, jclass cls, jint k, jint p,
+                                                                          jint s) {
+  (void)cls;
+  hrs_codec* c = NULL;
+  hrs_status st = hrs_create_src(k, p, s, NULL, &c);
+  if (st != HRS_OK) {
+    throw_status(env, st, NULL);
+    return 0;
+  }
+  return (jlong)(intptr_t)c;
+}
+
+JNIEXPORT jintArray JNICALL Java_io_hops_erasure_1coding_HrsNative_locationsToRead(JNIEnv* env, jclass cls, jlong h,
+                                                                                  jintArray erased) {
+  (void)cls;
+  hrs_codec* c = (hrs_codec*)(intptr_t)h;
+  const jsize ne = (*env)->GetArrayLength(env, erased);
+  jint* e = (*env)->GetIntArrayElements(env, erased, NULL);
+  int out[256];
+  int m = 0;
+  hrs_status st = hrs_locations_to_read_list(c, (const int*)e, ne, out, &m);
+  (*env)->ReleaseIntArrayElements(env, erased, e, JNI_ABORT);
+  if (st != HRS_OK) {
+    throw_status(env, st, c);
+    return NULL;
+  }
+  jintArray r = (*env)->NewIntArray(env, m);
+  if (r) (*env)->SetIntArrayRegion(env, r, 0, m, (const jint*)out);
+  return r;
+}
+
 JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_destroy(JNIEnv* env, jclass cls,
                                                                                      jlong h) {
   (void)env;

@@ -534,3 +534,218 @@ int orc_nrs_decode_bulk(int k, int p, uint8_t* const* read_bufs, uint8_t* const*
   free(outs); free(real); free(dec); free(inv); free(tmp); free(enc); free(decodeIndex); free(mod); free(in);
   return st;
 }
+
+/* ------------------------------------------- SimpleRegeneratingCode (src) */
+
+typedef struct {
+  int k, p, s, r, d, n;
+  int gen[256];
+  int ngen;
+  int pp[256];       /* primitivePower */
+  int* groups[256];  /* groupsTable */
+  int gsize[256];
+} src_code;
+
+static int src_group(const src_code* c, int loc) { /* getSRCGroup, :415-426 */
+  if (0 <= loc && loc < c->s) return loc;
+  if (c->s <= loc && loc < c->k + c->p) return (loc - c->s) / c->d;
+  return -1;
+}
+
+static int src_neighbors(const src_code* c, int loc, int* out) { /* getSRCGroupNeighbors, :371-409 */
+  int limit = c->k + c->p, m = 0;
+  int group = src_group(c, loc);
+  if (group < c->s) {
+    if (group != loc) out[m++] = group;
+    for (int i = c->s + group * c->d; i < c->s + (group + 1) * c->d; i++)
+      if (i != loc) out[m++] = i;
+  } else {
+    for (int i = 0; i < c->s; i++) out[m++] = i;
+    for (int i = c->s + group * c->d; i < limit; i++)
+      if (i != loc) out[m++] = i;
+  }
+  return m;
+}
+
+int orc_src_params(int k, int p, int s_in, int* s, int* r, int* d) { /* init, :70-114 */
+  int ss = s_in, rr = p - s_in;
+  int dd = (k + rr + ss) / (ss + 1); /* ceil((k + rr) / (ss + 1)) */
+  dd = (int)((k + rr + ss) / (ss + 1));
+  while (dd * ss >= k + rr) {
+    ss--;
+    rr++;
+    dd = (k + rr + ss) / (ss + 1);
+  }
+  *s = ss;
+  *r = rr;
+  *d = dd;
+  return 0;
+}
+
+static void src_init(src_code* c, int k, int p, int s_in) {
+  c->k = k;
+  c->p = p;
+  c->n = k + p;
+  orc_src_params(k, p, s_in, &c->s, &c->r, &c->d);
+  for (int i = 0; i < k + c->r; i++) c->pp[i] = orc_gf_power(2, i);
+  int gen[256] = {1}, ng = 1, poly[2], tmp[256];
+  for (int i = 0; i < c->r; i++) {
+    poly[0] = c->pp[i];
+    poly[1] = 1;
+    orc_gf_poly_mul(gen, ng, poly, 2, tmp);
+    ng += 1;
+    memcpy(gen, tmp, sizeof(int) * (size_t)ng);
+  }
+  memcpy(c->gen, gen, sizeof(int) * (size_t)ng);
+  c->ngen = ng;
+  for (int i = 0; i < c->n; i++) {
+    c->groups[i] = (int*)malloc(sizeof(int) * (size_t)c->n);
+    c->gsize[i] = src_neighbors(c, i, c->groups[i]);
+  }
+}
+
+static void src_free(src_code* c) {
+  for (int i = 0; i < c->n; i++) free(c->groups[i]);
+}
+
+static void src_encode(const src_code* c, const int* message, int* parity) { /* encode, :116-157 */
+  int buf[512];
+  for (int i = 0; i < c->r; i++) buf[i] = 0;
+  for (int i = 0; i < c->k; i++) buf[i + c->r] = message[i];
+  orc_gf_remainder(buf, c->r + c->k, c->gen, c->ngen);
+  for (int i = 0; i < c->r; i++) parity[i + c->s] = buf[i];
+  for (int i = 0; i < c->k; i++) buf[i + c->r] = message[i];
+  for (int i = 0; i < c->s; i++) {
+    parity[i] = 0;
+    for (int j = c->d * i; j < c->d * (i + 1); j++) parity[i] = buf[j] ^ parity[i];
+  }
+}
+
+void orc_src_encode(int k, int p, int s_in, const int* message, int* parity) {
+  src_code c;
+  src_init(&c, k, p, s_in);
+  src_encode(&c, message, parity);
+  src_free(&c);
+}
+
+/* decodeReedSolomon, :162-182; -1 if more erasures than errSignature holds */
+static int src_decode_rs(const src_code* c, int* data, const int* erased, int ne, int* values) {
+  if (ne == 0) return 0;
+  if (ne > c->r) return -1;
+  int sig[256];
+  for (int i = 0; i < ne; i++) data[erased[i]] = 0;
+  for (int i = 0; i < ne; i++) {
+    sig[i] = c->pp[erased[i]];
+    values[i] = orc_gf_substitute(data, c->r + c->k, c->pp[i]);
+  }
+  orc_gf_solve_vandermonde(sig, values, ne);
+  return 0;
+}
+
+static int src_conflict(const src_code* c, const int* locs, int n) { /* groupConflict, :432-453 */
+  int groups[257] = {0};
+  for (int i = 0; i < n; i++)
+    if (locs[i] < c->s) {
+      groups[c->s] = 1;
+      break;
+    }
+  for (int i = 0; i < n; i++)
+    if (groups[src_group(c, locs[i])]++ > 0) return 1;
+  return 0;
+}
+
+static int src_decode5(const src_code* c, int* data, const int* erased, int ne, int* values, const int* to_read,
+                       int nr, const int* ntr, int nn) { /* decode 5-arg, :194-277 */
+  if (ne == 1) {
+    values[0] = 0;
+    for (int i = 0; i < nr; i++) values[0] = data[to_read[i]] ^ values[0];
+    return 0;
+  }
+  if (!src_conflict(c, erased, ne)) {
+    for (int i = 0; i < ne; i++) {
+      int one = erased[i], v = 0;
+      src_decode5(c, data, &one, 1, &v, c->groups[erased[i]], c->gsize[erased[i]], NULL, 0);
+      values[i] = v;
+    }
+    return 0;
+  }
+  int dataRS[512], eRS[256], vRS[256], m = 0;
+  for (int i = 0; i < c->r + c->k; i++) dataRS[i] = data[i + c->s];
+  for (int i = 0; i < nn; i++)
+    if (ntr[i] >= c->s) eRS[m++] = ntr[i] - c->s;
+  if (src_decode_rs(c, dataRS, eRS, m, vRS) != 0) return -1;
+  for (int i = 0; i < m; i++) data[c->s + eRS[i]] = vRS[i];
+  for (int i = 0; i < ne; i++)
+    if (erased[i] < c->s) {
+      int par = erased[i];
+      data[par] = 0;
+      for (int j = 0; j < c->gsize[par]; j++) data[par] = data[c->groups[par][j]] ^ data[par];
+    }
+  for (int i = 0; i < ne; i++) values[i] = data[erased[i]];
+  return 0;
+}
+
+int orc_src_decode5(int k, int p, int s_in, int* data, const int* erased, int ne, int* values, const int* to_read,
+                    int nr, const int* ntr, int nn) {
+  src_code c;
+  src_init(&c, k, p, s_in);
+  int st = src_decode5(&c, data, erased, ne, values, to_read, nr, ntr, nn);
+  src_free(&c);
+  return st;
+}
+
+int orc_src_locations_to_read(int k, int p, int s_in, const int* erased, int ne, int* out) { /* :300-366 */
+  src_code c;
+  src_init(&c, k, p, s_in);
+  int m = 0;
+  if (ne == 1) {
+    for (int i = 0; i < c.gsize[erased[0]]; i++) out[m++] = c.groups[erased[0]][i];
+  } else if (!src_conflict(&c, erased, ne)) {
+    for (int e = 0; e < ne; e++)
+      for (int i = 0; i < c.gsize[erased[e]]; i++) {
+        int loc = c.groups[erased[e]][i], dup = 0;
+        for (int j = 0; j < m; j++) dup |= out[j] == loc;
+        if (!dup) out[m++] = loc;
+      }
+  } else {
+    for (int loc = c.s; loc < c.n; loc++) {
+      int bad = 0;
+      for (int i = 0; i < ne; i++) bad |= erased[i] == loc;
+      if (!bad) {
+        out[m++] = loc;
+        if (m == k) break;
+      }
+    }
+    if (m != k) m = -1;
+  }
+  src_free(&c);
+  return m;
+}
+
+void orc_src_encode_bulk(int k, int p, int s_in, uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  src_code c; /* ErasureCode.encodeBulk, :136-156 */
+  src_init(&c, k, p, s_in);
+  int data[256], code[256];
+  for (size_t j = 0; j < len; j++) {
+    for (int i = 0; i < p; i++) code[i] = 0;
+    for (int i = 0; i < k; i++) data[i] = inputs[i][j];
+    src_encode(&c, data, code);
+    for (int i = 0; i < p; i++) outputs[i][j] = (uint8_t)code[i];
+  }
+  src_free(&c);
+}
+
+int orc_src_decode_bulk(int k, int p, int s_in, uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                        const int* erased, int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len) {
+  src_code c; /* ErasureCode.decodeBulk, :162-181 */
+  src_init(&c, k, p, s_in);
+  int in[256], out[256], st = 0;
+  for (size_t idx = 0; idx < len && st == 0; idx++) {
+    for (int i = 0; i < ne; i++) out[i] = 0;
+    for (int i = 0; i < k + p; i++) in[i] = read_bufs[i] ? read_bufs[i][idx] : 0;
+    st = src_decode5(&c, in, erased, ne, out, to_read, nr, ntr, nn);
+    for (int i = 0; i < ne; i++) write_bufs[i][idx] = (uint8_t)out[i];
+  }
+  src_free(&c);
+  return st;
+}

@@ -87,6 +87,23 @@ void orc_nrs_encode_bulk(int k, int p, uint8_t* const* inputs, uint8_t* const* o
 int orc_nrs_decode_bulk(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
                         int ne, const int* not_to_read, int nn, size_t len);
 
+/* SimpleRegeneratingCode (the `src` codec, SimpleRegeneratingCode.java:28-482),
+ * with ErasureCode's default bulk loops (ErasureCode.java:136-181). s_in is
+ * the codec's parity_length_src; the init adjustment loop (:70-90) may lower it.
+ * Locations: [SRC parities 0..s-1, RS parities s..p-1, data p..p+k-1]. */
+int orc_src_params(int k, int p, int s_in, int* s, int* r, int* d);
+void orc_src_encode(int k, int p, int s_in, const int* message, int* parity);
+/* 5-arg decode of one symbol column; returns -1 where the Java would throw
+ * (ArrayIndexOutOfBounds of errSignature). data is modified as in the Java. */
+int orc_src_decode5(int k, int p, int s_in, int* data, const int* erased, int ne, int* values, const int* to_read,
+                    int nr, const int* ntr, int nn);
+/* locationsToReadForDecode; returns the count written to out (capacity k+p)
+ * or -1 for TooManyErasedLocations. */
+int orc_src_locations_to_read(int k, int p, int s_in, const int* erased, int ne, int* out);
+void orc_src_encode_bulk(int k, int p, int s_in, uint8_t* const* inputs, uint8_t* const* outputs, size_t len);
+int orc_src_decode_bulk(int k, int p, int s_in, uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                        const int* erased, int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len);
+
 #ifdef __cplusplus
 }
 #endif

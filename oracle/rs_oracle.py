@@ -66,6 +66,12 @@ def lib():
             "orc_nrs_encode_matrix": ([I, I, ctypes.c_void_p], None),
             "orc_nrs_encode_bulk": ([I, I, PP, PP, S], None),
             "orc_nrs_decode_bulk": ([I, I, PP, PP, IP, I, IP, I, S], I),
+            "orc_src_params": ([I, I, I, IP, IP, IP], I),
+            "orc_src_encode": ([I, I, I, IP, IP], None),
+            "orc_src_decode5": ([I, I, I, IP, IP, I, IP, IP, I, IP, I], I),
+            "orc_src_locations_to_read": ([I, I, I, IP, I, IP], I),
+            "orc_src_encode_bulk": ([I, I, I, PP, PP, S], None),
+            "orc_src_decode_bulk": ([I, I, I, PP, PP, IP, I, IP, I, IP, I, S], I),
         }
         for name, (args, res) in sigs.items():
             f = getattr(_lib, name)
@@ -265,6 +271,53 @@ def nrs_decode_bulk(k, p, read_bufs, erased, not_to_read):
                                    _ints(not_to_read), len(not_to_read), L)
     assert st == 0
     return outs
+
+
+# ------------------------------------------- SimpleRegeneratingCode (src)
+
+def src_params(k, p, s):
+    """(s, r, d) after SimpleRegeneratingCode.init's adjustment loop."""
+    a, b, c = _ints([0]), _ints([0]), _ints([0])
+    lib().orc_src_params(k, p, s, a, b, c)
+    return a[0], b[0], c[0]
+
+
+def src_encode(k, p, s, message):
+    par = _ints([0] * p)
+    lib().orc_src_encode(k, p, s, _ints(message), par)
+    return list(par)[:p]
+
+
+def src_decode5(k, p, s, data, erased, to_read, not_to_read):
+    """One symbol column; None where the Java would throw."""
+    d = _ints(data)
+    vals = _ints([0] * len(erased))
+    st = lib().orc_src_decode5(k, p, s, d, _ints(erased), len(erased), vals, _ints(to_read), len(to_read),
+                               _ints(not_to_read), len(not_to_read))
+    return None if st else list(vals)[: len(erased)]
+
+
+def src_locations_to_read(k, p, s, erased):
+    """Ordered list, or None for TooManyErasedLocations."""
+    out = _ints([0] * (k + p))
+    m = lib().orc_src_locations_to_read(k, p, s, _ints(erased), len(erased), out)
+    return None if m < 0 else list(out)[:m]
+
+
+def src_encode_bulk(k, p, s, inputs):
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    outs = [np.zeros(rows[0].size, dtype=np.uint8) for _ in range(p)]
+    lib().orc_src_encode_bulk(k, p, s, _rowptrs(rows), _rowptrs(outs), rows[0].size)
+    return outs
+
+
+def src_decode_bulk(k, p, s, read_bufs, erased, to_read, not_to_read):
+    rows = [None if r is None else np.ascontiguousarray(r, dtype=np.uint8) for r in read_bufs]
+    L = max(r.size for r in rows if r is not None)
+    outs = [np.zeros(L, dtype=np.uint8) for _ in erased]
+    st = lib().orc_src_decode_bulk(k, p, s, _rowptrs(rows), _rowptrs(outs), _ints(erased), len(erased),
+                                   _ints(to_read), len(to_read), _ints(not_to_read), len(not_to_read), L)
+    return None if st else outs
 
 
 # Raw entry points for the CPU baseline (pointer arrays prepared once).

@@ -11,7 +11,9 @@
 //    (StripeReader.java:106-124); code.decodeBulk(...) per round (:352-353);
 //    the repaired block's CRC32 compared with the stored one (:222-229).
 //
-// Usage: codec_harness [--host-only] [--xor | --nrs] k p blockSize bufSize nerased seed
+// Usage: codec_harness [--host-only] [--xor | --nrs | --src=S] k p blockSize bufSize nerased seed
+// --src=S drives SimpleRegeneratingCode with S SRC parities (local groups;
+// a pattern the code cannot repair is redrawn).
 // --nrs drives NativeReedSolomonCode semantics: rounds are checked against the
 // oracle's orc_nrs_decode_bulk, and the repaired CRC against the block the Java
 // actually returns in writeBufs[i] (the i-th not-to-read location in Apache
@@ -79,7 +81,8 @@ int host_only_checks(int k, int p) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  bool host_only = false, use_xor = false, use_nrs = false;
+  bool host_only = false, use_xor = false, use_nrs = false, use_src = false;
+  int src_s = 0;
   std::vector<std::string> pos;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -89,6 +92,10 @@ int main(int argc, char** argv) {
       use_xor = true;
     else if (a == "--nrs")
       use_nrs = true;
+    else if (a.rfind("--src=", 0) == 0) {
+      use_src = true;
+      src_s = atoi(a.c_str() + 6);
+    }
     else
       pos.push_back(a);
   }
@@ -107,6 +114,8 @@ int main(int argc, char** argv) {
       code.reset(new hrs::HipXORCode(k, 0));
     else if (use_nrs)
       code.reset(new hrs::HipNativeReedSolomonCode(k, p, 0));
+    else if (use_src)
+      code.reset(new hrs::HipSimpleRegeneratingCode(k, p, src_s, 0));
     else
       code.reset(new hrs::HipReedSolomonCode(k, p, 0));
 
@@ -143,6 +152,8 @@ int main(int argc, char** argv) {
         orc_xor_encode_bulk(k, cpp.data(), refp[0], len);
       else if (use_nrs)
         orc_nrs_encode_bulk(k, p, cpp.data(), refp.data(), len);
+      else if (use_src)
+        orc_src_encode_bulk(k, p, src_s, cpp.data(), refp.data(), len);
       else
         orc_rs_encode_bulk(k, p, cpp.data(), refp.data(), len);
       for (int r = 0; r < p; ++r) {
@@ -153,15 +164,23 @@ int main(int argc, char** argv) {
     }
 
     // ---- lose blocks, Decoder.fixErasedBlockImpl
-    std::vector<int> erased_list;
+    std::vector<int> erased_list, to_read_list;
     uint64_t s = seed;
-    while (static_cast<int>(erased_list.size()) < nerased) {
-      int loc = static_cast<int>(splitmix(s) % n);
-      bool dup = false;
-      for (int e : erased_list) dup |= e == loc;
-      if (!dup) erased_list.push_back(loc);
+    for (;;) {  // SRC: redraw patterns its local groups + RS part cannot repair
+      erased_list.clear();
+      while (static_cast<int>(erased_list.size()) < nerased) {
+        int loc = static_cast<int>(splitmix(s) % n);
+        bool dup = false;
+        for (int e : erased_list) dup |= e == loc;
+        if (!dup) erased_list.push_back(loc);
+      }
+      try {
+        to_read_list = code->locationsToReadForDecode(erased_list);
+        break;
+      } catch (const hrs::TooManyErasedLocations&) {
+        if (!use_src) throw;
+      }
     }
-    std::vector<int> to_read_list = code->locationsToReadForDecode(erased_list);
     auto contains = [](const std::vector<int>& v, int x) {
       for (int y : v)
         if (y == x) return true;
@@ -212,6 +231,16 @@ int main(int argc, char** argv) {
         rep_mismatch += std::memcmp(wb[i].data(), stripe_row(expect[i]) + off, len) != 0;
         rep_crc[i] = crc(rep_crc[i], wb[i].data(), len);
       }
+      if (use_src) {  // the reference's own output for this round
+        std::vector<std::vector<uint8_t>> ref(ne, std::vector<uint8_t>(len));
+        std::vector<uint8_t*> refp(ne);
+        for (int i = 0; i < ne; ++i) refp[i] = ref[i].data();
+        if (orc_src_decode_bulk(k, p, src_s, rp.data(), refp.data(), erased_arr.data(), ne, to_read_arr.data(),
+                                static_cast<int>(to_read_arr.size()), ntr_arr.data(),
+                                static_cast<int>(ntr_arr.size()), len) != 0)
+          ++rep_mismatch;
+        for (int i = 0; i < ne; ++i) rep_mismatch += std::memcmp(ref[i].data(), wb[i].data(), len) != 0;
+      }
       if (use_nrs) {  // the reference's own output for this round
         std::vector<std::vector<uint8_t>> ref(ne, std::vector<uint8_t>(len));
         std::vector<uint8_t*> refp(ne);
@@ -229,7 +258,7 @@ int main(int argc, char** argv) {
       crc_bad += stored != rep_crc[i];
     }
     const bool ok = mismatches == 0 && rep_mismatch == 0 && crc_bad == 0;
-    printf("{\"code\": \"%s\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"erased\": [", use_xor ? "xor" : use_nrs ? "nrs" : "rs",
+    printf("{\"code\": \"%s\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"erased\": [", use_xor ? "xor" : use_nrs ? "nrs" : use_src ? "src" : "rs",
            k, p, block, buf);
     for (int i = 0; i < ne; ++i) printf("%s%d", i ? ", " : "", erased_arr[i]);
     printf("], \"quirk\": %s, \"encode_round_mismatches\": %zu, \"repair_mismatches\": %zu, \"crc_mismatches\": %zu, "

@@ -54,3 +54,12 @@ def test_harness_nrs(cuda, nerased, seed):
     # of the block the Java hands back (res["quirk"]: not the erased one)
     rc, res = run("--nrs", 10, 4, 3 << 20, 1 << 20, nerased, seed)
     assert rc == 0 and res["ok"], res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nerased,seed", [(1, 3), (2, 4), (2, 9), (3, 5), (4, 6)])
+def test_harness_src(cuda, nerased, seed):
+    # SimpleRegeneratingCode(10, 6, 2): local-group and RS repairs, each round
+    # equal to the oracle's transcription, repaired CRCs equal to the stored ones
+    rc, res = run("--src=2", 10, 6, 3 << 20, 1 << 20, nerased, seed)
+    assert rc == 0 and res["ok"], res

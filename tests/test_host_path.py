@@ -1,0 +1,46 @@
+"""The synchronous host-buffer calls (hrs_encode / hrs_decode, the JNI path)
+through the pipelined pinned-staging host path: rows longer than one chunk
+(HRS_HOST_CHUNK, default 512 KiB), ragged last chunks, several calls in a row
+(slot reuse), bit-exact against the oracle."""
+import numpy as np
+import pytest
+
+from lambdafs_amd import HipNativeReedSolomonCode, HipReedSolomonCode, HipXORCode
+from oracle import rs_oracle as C
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("L", [(3 << 20) + 777, (2 << 20), 4096 + 5, 1])
+def test_host_encode_decode_multi_chunk(cuda, L):
+    k, p = 10, 4
+    n = k + p
+    code = HipReedSolomonCode(k, p, zero_inputs_after_encode=False)
+    rng = np.random.default_rng(L % 1000)
+    for call in range(3):
+        data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        par = [np.zeros(L, np.uint8) for _ in range(p)]
+        code.encodeBulk(data, par)
+        ref = C.encode_bulk(k, p, data)
+        assert all((a == b).all() for a, b in zip(par, ref)), call
+        stripe = par + data
+        erased = [p + call, 1]
+        to_read = sorted(code.locationsToReadForDecode(erased))
+        ntr = [x for x in range(n) if x not in to_read]
+        out = [np.zeros(L, np.uint8) for _ in erased]
+        code.decodeBulk([stripe[i] if i in to_read else None for i in range(n)], out, erased, to_read, ntr)
+        assert all((o == stripe[e]).all() for o, e in zip(out, erased)), call
+
+
+def test_host_nrs_and_xor_multi_chunk(cuda):
+    L = (2 << 20) + 3
+    rng = np.random.default_rng(9)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(10)]
+    nrs = HipNativeReedSolomonCode(10, 4)
+    par = [np.zeros(L, np.uint8) for _ in range(4)]
+    nrs.encodeBulk(data, par)
+    assert all((a == b).all() for a, b in zip(par, C.nrs_encode_bulk(10, 4, data)))
+    xor = HipXORCode(10, 1)
+    xp = [np.zeros(L, np.uint8)]
+    xor.encodeBulk(data, xp)
+    assert (xp[0] == C.xor_encode_bulk(10, data)).all()

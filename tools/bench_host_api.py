@@ -52,6 +52,8 @@ def main():
     td = (time.perf_counter() - t0) / args.calls
     print(json.dumps({
         "path": "synchronous host-buffer calls (hrs_encode / hrs_decode), pageable rows, 1 call per stripe",
+        "copy_threads": os.environ.get("HRS_HOST_THREADS", "2 (default)"),
+        "chunk_bytes": os.environ.get("HRS_HOST_CHUNK", "524288 (default)"),
         "encodeBulk_ms_per_call": round(te * 1e3, 3),
         "encodeBulk_GiBps_user_data": round(k * L / GiB / te, 2),
         "encodeBulk_GBps_pcie": round((k + p) * L / te / 1e9, 2),
