@@ -306,7 +306,10 @@ def main():
             "random_location_decode": {
                 "what": "config 3 second run: one seeded random lost location per stripe, one batch launch",
                 "launch_ms": stats(rand_ms),
+                "kernel": "batch_bitsliced_kernel<1,12>",
                 "GBps_algorithmic": round((k + 1) * L * S / (float(np.median(rand_ms)) * 1e-3) / 1e9, 1),
+                "algorithmic_bytes_per_launch": (k + 1) * L * S,
+                "traffic": load_traffic("batch_bitsliced_kernel<1,12>"),
                 "GiBps_user_per_gpu": round(k * L * S / GiB / (float(np.median(rand_ms)) * 1e-3), 3),
             },
             "copy_peak": peak,
