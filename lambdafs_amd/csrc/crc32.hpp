@@ -16,6 +16,17 @@ namespace crc {
 
 constexpr uint32_t kPoly = 0xEDB88320u;  // reflected 0x04C11DB7
 
+// Window decomposition of the GPU kernels (hrs_crc.hip), shared with the CPU
+// model (tests/cpp/crc_model.cpp): a window is kPieces chunks of 1 KiB; lane
+// l of the window's wave owns the 16-byte piece at q * 1024 + 16 l of every
+// chunk q (so each load instruction is one contiguous 1 KiB wave access).
+// Its piece CRCs join in chunk order with Z_1024, and a 6-level lane tree
+// joins the lanes with Z_{16 * 2^t}.
+constexpr int kChunkBytes = 1024;
+constexpr int kPieceBytes = 16;
+constexpr int kPieces = 32;
+constexpr uint64_t kWindowBytes = static_cast<uint64_t>(kChunkBytes) * kPieces;  // 32 KiB
+
 struct ByteTable {
   uint32_t t[256];
 };

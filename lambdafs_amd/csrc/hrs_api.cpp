@@ -787,9 +787,9 @@ hrs_status crc_window_tables(hrs_codec* c) {
   for (int j = 0; j < 4; ++j)
     for (int v = 0; v < 256; ++v)
       for (int r = 0; r < hrs::kCrcRep; ++r) h[(j * 256 + v) * hrs::kCrcRep + r] = sl.s[j].t[v];
-  cr::to_tables(cr::zeros(16), &h[hrs::kCrcSliceWords]);  // joins the lane's 16-byte chains
-  for (int t = 0; t < 6; ++t)
-    cr::to_tables(cr::zeros(static_cast<uint64_t>(hrs::kCrcLaneBytes) << t), &h[hrs::kCrcSliceWords + (1 + t) * 1024]);
+  cr::to_tables(cr::zeros(cr::kChunkBytes), &h[hrs::kCrcSliceWords]);  // joins a lane's pieces, chunk to chunk
+  for (int t = 0; t < 6; ++t)  // lane tree: lane l + 2^t is 16 * 2^t bytes later
+    cr::to_tables(cr::zeros(static_cast<uint64_t>(cr::kPieceBytes) << t), &h[hrs::kCrcSliceWords + (1 + t) * 1024]);
   return upload(c, h, &c->crc_tables_a);
 }
 

@@ -4,17 +4,19 @@
 
 #include <cstdint>
 
+#include "crc32.hpp"
+
 namespace hrs {
 
-constexpr int kCrcWindow = 4096;     // bytes per wave task
-constexpr int kCrcLaneBytes = 64;    // contiguous bytes per lane (16 words)
-constexpr int kCrcRep = 4;           // slicing tables replicated across LDS banks
-constexpr int kCrcChains = 4;        // independent 16-byte chains per lane (ILP)
-constexpr int kCrcBlocksPerCU = 3;
+constexpr int kCrcWindow = static_cast<int>(crc::kWindowBytes);  // bytes per wave task (32 KiB)
+constexpr int kCrcRep = 32;          // slicing tables replicated: lane l reads copy l % 32 (its own bank)
+constexpr int kCrcGroup = 8;         // chunks loaded and chained together (ILP)
+constexpr int kCrcBlockThreads = 1024;  // 16 waves share one table image per CU
 constexpr int kCrcMaxRows = 32;      // rows per window launch
-constexpr int kCrcSliceWords = 4 * 256 * kCrcRep;           // 16 KiB
-constexpr int kCrcLdsWordsA = kCrcSliceWords + 7 * 1024;    // + Z_16, Z_{64*2^t} t = 0..5 (28 KiB)
-constexpr int kCrcLdsWordsB = 9 * 1024;                     // Z_4096, 6 tree levels, Z_tail, Z_len (36 KiB)
+constexpr int kCrcSliceWords = 4 * 256 * kCrcRep;           // 128 KiB
+constexpr int kCrcLdsWordsA = kCrcSliceWords + 7 * 1024;    // + Z_1024, Z_{16*2^t} t = 0..5 (156 KiB)
+constexpr int kCrcLdsWordsB = 9 * 1024;                     // Z_window, 6 tree levels, Z_tail, Z_len (36 KiB)
+constexpr int kCrcFoldBlocksPerCU = 3;
 
 struct CrcWinArgs {
   const uint8_t* rows[kCrcMaxRows];
@@ -24,8 +26,8 @@ struct CrcWinArgs {
   int pad_;
   uint64_t stride;  // bytes between stripes
   uint64_t len;
-  uint64_t nwin;    // full 4 KiB windows per row
-  uint64_t tail;    // len - nwin * 4096
+  uint64_t nwin;    // full windows per row
+  uint64_t tail;    // len - nwin * kCrcWindow
   uint64_t nstripes;
   uint32_t* raw;
   const uint32_t* tables;  // kCrcLdsWordsA words (device)

@@ -1,8 +1,10 @@
 // CPU model of the CRC-32 kernels (lambdafs_amd/csrc/hrs_crc.hip): the same
-// tables (crc32.hpp) and the same decomposition — 64 lanes x 64 B slicing-by-4
-// per 4 KiB window (four 16-byte chains per lane joined by Z_16), a 6-level lane tree with Z_{64*2^t}, the window fold with
-// G windows per lane + Z_{4096*G*2^t} tree, the right-aligned tail window and
-// CRC32.update chaining — emulated lane by lane and checked against zlib.
+// tables (crc32.hpp) and the same decomposition — per 32 KiB window, lane l
+// owns the 16-byte piece at q*1024 + 16l of each 1 KiB chunk q (slicing-by-4),
+// joins its pieces in chunk order with Z_1024, then a 6-level lane tree with
+// Z_{16*2^t}; the window fold with G windows per lane + Z_{window*G*2^t}
+// tree, the right-aligned tail window and CRC32.update chaining — emulated
+// lane by lane and checked against zlib.
 #include <zlib.h>
 
 #include <cstdio>
@@ -22,28 +24,27 @@ static std::vector<uint32_t> tab(uint64_t n) {
   return t;
 }
 
-static std::vector<uint32_t> z16 = tab(16);
+static std::vector<uint32_t> zchunk = tab(kChunkBytes);
+static const int64_t W = static_cast<int64_t>(kWindowBytes);
 
 static uint32_t window_raw(const Slice4& sl, const std::vector<std::vector<uint32_t>>& tree, const uint8_t* p,
                            int64_t start, int64_t lo, int64_t end) {
   uint32_t c[64];
   for (int lane = 0; lane < 64; ++lane) {
-    uint32_t w[16];
-    for (int j = 0; j < 16; ++j) {
-      w[j] = 0;
-      for (int b = 0; b < 4; ++b) {
-        int64_t pos = start + lane * 64 + 4 * j + b;
-        if (pos >= lo && pos < end) w[j] |= (uint32_t)p[pos] << (8 * b);
+    uint32_t x = 0;
+    for (int q = 0; q < kPieces; ++q) {
+      uint32_t ch = 0;  // the 16-byte piece at q*1024 + 16*lane
+      for (int j = 0; j < 4; ++j) {
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b) {
+          const int64_t pos = start + (int64_t)q * kChunkBytes + lane * kPieceBytes + 4 * j + b;
+          if (pos >= lo && pos < end) w |= (uint32_t)p[pos] << (8 * b);
+        }
+        const uint32_t y = ch ^ w;
+        ch = sl.s[3].t[y & 255] ^ sl.s[2].t[(y >> 8) & 255] ^ sl.s[1].t[(y >> 16) & 255] ^ sl.s[0].t[y >> 24];
       }
+      x = q == 0 ? ch : (zmul(zchunk, x) ^ ch);
     }
-    uint32_t ch[4] = {0, 0, 0, 0};  // four 16-byte chains, joined with Z_16
-    for (int step = 0; step < 4; ++step)
-      for (int q = 0; q < 4; ++q) {
-        uint32_t x = ch[q] ^ w[4 * q + step];
-        ch[q] = sl.s[3].t[x & 255] ^ sl.s[2].t[(x >> 8) & 255] ^ sl.s[1].t[(x >> 16) & 255] ^ sl.s[0].t[x >> 24];
-      }
-    uint32_t x = ch[0];
-    for (int q = 1; q < 4; ++q) x = zmul(z16, x) ^ ch[q];
     c[lane] = x;
   }
   for (int lvl = 0; lvl < 6; ++lvl) {
@@ -57,20 +58,20 @@ static uint32_t window_raw(const Slice4& sl, const std::vector<std::vector<uint3
 int main() {
   const Slice4 sl = make_slice4();
   std::vector<std::vector<uint32_t>> tree;
-  for (int t = 0; t < 6; ++t) tree.push_back(tab(64ull << t));
+  for (int t = 0; t < 6; ++t) tree.push_back(tab((uint64_t)kPieceBytes << t));
   int bad = 0, cases = 0;
   uint64_t seed = 1;
-  for (size_t len : {0ul, 1ul, 63ul, 64ul, 4095ul, 4096ul, 4097ul, 8192ul + 5, 65536ul * 3 + 1000, 1ul << 20,
-                     (1ul << 20) + 4096 * 70 + 33}) {
+  for (size_t len : {0ul, 1ul, 63ul, 64ul, 4095ul, 4096ul, 32767ul, 32768ul, 32769ul, 65536ul + 5,
+                     65536ul * 3 + 1000, 1ul << 20, (1ul << 20) + 32768 * 70 + 33, 32768ul * 64 * 2 + 17}) {
     std::vector<uint8_t> d(len);
     for (auto& x : d) x = (uint8_t)((seed = seed * 6364136223846793005ull + 1442695040888963407ull) >> 56);
-    const uint64_t nwin = len / 4096, tail = len % 4096, G = (nwin + 63) / 64;
+    const uint64_t nwin = len / W, tail = len % W, G = (nwin + 63) / 64;
     std::vector<uint32_t> raw(nwin + 1);
-    for (uint64_t w = 0; w < nwin; ++w) raw[w] = window_raw(sl, tree, d.data(), w * 4096, w * 4096, (w + 1) * 4096);
-    if (tail) raw[nwin] = window_raw(sl, tree, d.data(), (int64_t)len - 4096, nwin * 4096, len);
-    auto zw = tab(4096), ztail = tab(tail), zlen = tab(len);
+    for (uint64_t w = 0; w < nwin; ++w) raw[w] = window_raw(sl, tree, d.data(), w * W, w * W, (w + 1) * W);
+    if (tail) raw[nwin] = window_raw(sl, tree, d.data(), (int64_t)len - W, nwin * W, len);
+    auto zw = tab(W), ztail = tab(tail), zlen = tab(len);
     std::vector<std::vector<uint32_t>> ft;
-    for (int t = 0; t < 6; ++t) ft.push_back(tab(4096 * G << t));
+    for (int t = 0; t < 6; ++t) ft.push_back(tab(W * G << t));
     for (uint32_t crc_in : {0u, 0xDEADBEEFu}) {
       uint32_t c[64];
       const int64_t pad = (int64_t)G * 64 - (int64_t)nwin;
