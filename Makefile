@@ -8,7 +8,7 @@ CC       ?= gcc
 
 LIB      := lambdafs_amd/libhrs.so
 ORACLE   := oracle/liboracle.so
-HDRS     := include/hrs.h lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
+HDRS     := include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
             lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
 
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model
@@ -27,7 +27,11 @@ build/hrs_crc.o: lambdafs_amd/csrc/hrs_crc.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): build/hrs_api.o build/hrs_kernels.o build/hrs_crc.o
+build/hrs_fused.o: lambdafs_amd/csrc/hrs_fused.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): build/hrs_api.o build/hrs_kernels.o build/hrs_crc.o build/hrs_fused.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h

@@ -221,6 +221,19 @@ hrs_status hrs_apply_dev(hrs_codec* codec, const uint8_t* m, int nout, int nin,
 hrs_status hrs_crc32_dev(hrs_codec* codec, const uint8_t* const* rows, int nrows, size_t stride, size_t len,
                          size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, void* stream);
 
+/* Encode + CRC-32 in one pass (Encoder.encodeStripe with computeBlockChecksum:
+ * sourceChecksums over the read buffers, then encodeBulk, then parityChecksums
+ * over the write buffers; Encoder.java:408-450). Same rows as hrs_encode_dev;
+ * crc_out[s * (k + p) + r] = CRC32 of data row r (r < k) or of parity row r - k
+ * (r >= k) of stripe s, continuing from crc_in (same layout; NULL = fresh).
+ * rs / nrs codes with a compile-time kernel ((10,4), (6,3), (3,2), (12,4) rs;
+ * (10,4), (6,3) nrs), len a multiple of 32 KiB and 16-byte-aligned rows take
+ * one fused kernel (each cell read once); anything else runs hrs_encode_dev
+ * then the CRC pass, with identical results. Asynchronous on `stream`. */
+hrs_status hrs_encode_crc_dev(hrs_codec* codec, const uint8_t* const* in_rows, size_t in_stride,
+                              uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
+                              const uint32_t* crc_in, uint32_t* crc_out, void* stream);
+
 /* Kernel selection for tests and benchmarks: 0 = auto (default), 1 = force
  * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel. */
 hrs_status hrs_set_kernel_mode(hrs_codec* codec, int mode);

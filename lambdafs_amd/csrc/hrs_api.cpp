@@ -786,7 +786,7 @@ hrs_status crc_window_tables(hrs_codec* c) {
   const cr::Slice4 sl = cr::make_slice4();
   for (int j = 0; j < 4; ++j)
     for (int v = 0; v < 256; ++v)
-      for (int r = 0; r < hrs::kCrcRep; ++r) h[(j * 256 + v) * hrs::kCrcRep + r] = sl.s[j].t[v];
+      for (int r = 0; r < hrs::kCrcRep; ++r) h[hrs::crc_slice_word(j, v, r)] = sl.s[j].t[v];
   cr::to_tables(cr::zeros(cr::kChunkBytes), &h[hrs::kCrcSliceWords]);  // joins a lane's pieces, chunk to chunk
   for (int t = 0; t < 6; ++t)  // lane tree: lane l + 2^t is 16 * 2^t bytes later
     cr::to_tables(cr::zeros(static_cast<uint64_t>(cr::kPieceBytes) << t), &h[hrs::kCrcSliceWords + (1 + t) * 1024]);
@@ -820,6 +820,77 @@ hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, const uint32_t** out) {
   return HRS_OK;
 }
 
+// Raw-CRC scratch of at least `bytes` (the fold reads it after the window pass).
+hrs_status crc_scratch(hrs_codec* c, size_t bytes, hipStream_t s) {
+  bytes = std::max<size_t>(4, bytes);
+  if (c->crc_raw_bytes >= bytes) return HRS_OK;
+  if (c->crc_raw) {
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(c->crc_raw);
+    c->crc_raw = nullptr;
+    c->crc_raw_bytes = 0;
+  }
+  hipError_t e = hipMalloc(&c->crc_raw, bytes);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  c->crc_raw_bytes = bytes;
+  return HRS_OK;
+}
+
+// Folds the raw window CRCs of nsr (stripe, row) pairs into CRC32 values.
+hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s) {
+  const uint32_t* fold = nullptr;
+  hrs_status st = crc_fold_tables(c, len, &fold);
+  if (st != HRS_OK) return st;
+  hrs::CrcFoldArgs f{};
+  f.raw = c->crc_raw;
+  f.nwin = len / hrs::kCrcWindow;
+  f.tail = len % hrs::kCrcWindow;
+  f.nsr = nsr;
+  f.G = static_cast<int>((f.nwin + 63) / 64);
+  f.tables = fold;
+  f.crc_in = crc_in;
+  f.crc_out = crc_out;
+  hipError_t e = hrs::launch_crc_fold(f, hrs::device_cu_count(), s);
+  if (e != hipSuccess) return hip_fail(c, e, "crc fold launch");
+  return HRS_OK;
+}
+
+// CRC-32 of nrows rows per stripe, row r at rows[r] + stripe * strides[r]:
+// window pass + fold. crc_out[s * nrows + r].
+hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strides, int nrows, size_t len,
+                   size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s) {
+  hrs_status st = crc_window_tables(c);
+  if (st != HRS_OK) return st;
+  const uint64_t nwin = len / hrs::kCrcWindow, tail = len % hrs::kCrcWindow;
+  const uint64_t wpr = nwin + (tail ? 1 : 0);
+  st = crc_scratch(c, nstripes * nrows * wpr * 4, s);
+  if (st != HRS_OK) return st;
+  const int cus = hrs::device_cu_count();
+  bool aligned = true;
+  for (int r = 0; r < nrows; ++r) aligned &= aligned16(rows[r]) && strides[r] % 16 == 0;
+  if (wpr > 0) {
+    for (int r0 = 0; r0 < nrows; r0 += hrs::kCrcMaxRows) {
+      hrs::CrcWinArgs a{};
+      a.nrows = std::min(hrs::kCrcMaxRows, nrows - r0);
+      for (int r = 0; r < a.nrows; ++r) {
+        a.rows[r] = rows[r0 + r];
+        a.stride[r] = strides[r0 + r];
+      }
+      a.row0 = r0;
+      a.nrows_total = nrows;
+      a.len = len;
+      a.nwin = nwin;
+      a.tail = tail;
+      a.nstripes = nstripes;
+      a.raw = c->crc_raw;
+      a.tables = c->crc_tables_a;
+      hipError_t e = hrs::launch_crc_windows(a, aligned, cus, s);
+      if (e != hipSuccess) return hip_fail(c, e, "crc window launch");
+    }
+  }
+  return crc_fold(c, len, nstripes * nrows, crc_in, crc_out, s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -833,61 +904,67 @@ hrs_status hrs_crc32_dev(hrs_codec* c, const uint8_t* const* rows, int nrows, si
   if (nstripes == 0) return HRS_OK;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  hrs_status st = crc_window_tables(c);
-  if (st != HRS_OK) return st;
-  const uint32_t* fold = nullptr;
-  st = crc_fold_tables(c, len, &fold);
-  if (st != HRS_OK) return st;
-  const uint64_t nwin = len / hrs::kCrcWindow, tail = len % hrs::kCrcWindow;
-  const uint64_t wpr = nwin + (tail ? 1 : 0);
-  const size_t raw_bytes = std::max<size_t>(4, nstripes * nrows * wpr * 4);
-  if (c->crc_raw_bytes < raw_bytes) {
-    if (c->crc_raw) {
-      (void)hipStreamSynchronize(s);
-      (void)hipFree(c->crc_raw);
-      c->crc_raw = nullptr;
-      c->crc_raw_bytes = 0;
-    }
-    hipError_t e = hipMalloc(&c->crc_raw, raw_bytes);
-    if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", raw_bytes, hipGetErrorString(e));
-    c->crc_raw_bytes = raw_bytes;
-  }
-  const int cus = hrs::device_cu_count();
-  bool aligned = stride % 16 == 0;
-  for (int r = 0; r < nrows; ++r) aligned &= aligned16(rows[r]);
-  if (wpr > 0) {
-    for (int r0 = 0; r0 < nrows; r0 += hrs::kCrcMaxRows) {
-      hrs::CrcWinArgs a{};
-      a.nrows = std::min(hrs::kCrcMaxRows, nrows - r0);
-      for (int r = 0; r < a.nrows; ++r) a.rows[r] = rows[r0 + r];
-      a.row0 = r0;
-      a.nrows_total = nrows;
-      a.stride = stride;
-      a.len = len;
-      a.nwin = nwin;
-      a.tail = tail;
-      a.nstripes = nstripes;
-      a.raw = c->crc_raw;
-      a.tables = c->crc_tables_a;
-      hipError_t e = hrs::launch_crc_windows(a, aligned, cus, s);
-      if (e != hipSuccess) return hip_fail(c, e, "crc window launch");
-    }
-  }
-  hrs::CrcFoldArgs f{};
-  f.raw = c->crc_raw;
-  f.nwin = nwin;
-  f.tail = tail;
-  f.nsr = nstripes * nrows;
-  f.G = static_cast<int>((nwin + 63) / 64);
-  f.tables = fold;
-  f.crc_in = crc_in;
-  f.crc_out = crc_out;
-  hipError_t e = hrs::launch_crc_fold(f, cus, s);
-  if (e != hipSuccess) return hip_fail(c, e, "crc fold launch");
-  return HRS_OK;
+  std::vector<size_t> strides(nrows, stride);
+  return run_crc(c, rows, strides.data(), nrows, len, nstripes, crc_in, crc_out, static_cast<hipStream_t>(stream));
 }
 
+hrs_status hrs_encode_crc_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
+                              size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in,
+                              uint32_t* crc_out, void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!in_rows || !out_rows || !crc_out) return fail(c, HRS_EINVAL, "row or crc arrays are NULL");
+  const int k = c->k, p = c->p, n = c->n;
+  for (int i = 0; i < k; ++i)
+    if (!in_rows[i] && len) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
+  for (int o = 0; o < p; ++o)
+    if (!out_rows[o] && len) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  if (nstripes == 0) return HRS_OK;
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // one pass: a static (k, p) of rs / nrs, whole 32 KiB windows, 16-byte aligned rows
+  bool fused = (c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS) && c->kernel_mode == 0 && len > 0 &&
+               len % hrs::kCrcWindow == 0 && k <= hrs::kFusedMaxK && p <= hrs::kFusedMaxP &&
+               in_stride % 16 == 0 && out_stride % 16 == 0;
+  for (int i = 0; i < k && fused; ++i) fused &= aligned16(in_rows[i]);
+  for (int o = 0; o < p && fused; ++o) fused &= aligned16(out_rows[o]);
+  if (fused) {
+    hrs_status st = crc_window_tables(c);
+    if (st != HRS_OK) return st;
+    const uint64_t nwin = len / hrs::kCrcWindow;
+    st = crc_scratch(c, nstripes * n * nwin * 4, s);
+    if (st != HRS_OK) return st;
+    hrs::EncodeCrcArgs a{};
+    for (int i = 0; i < k; ++i) a.in[i] = in_rows[i];
+    for (int o = 0; o < p; ++o) a.out[o] = out_rows[o];
+    a.in_stride = in_stride;
+    a.out_stride = out_stride;
+    a.nwin = nwin;
+    a.nstripes = nstripes;
+    a.raw = c->crc_raw;
+    a.tables = c->crc_tables_a;
+    bool handled = false;
+    const int family = c->kind == HRS_CODE_NRS ? hrs::kStaticCauchy : hrs::kStaticRs;
+    hipError_t e = hrs::launch_encode_crc(family, k, p, a, hrs::device_cu_count(), s, &handled);
+    if (e != hipSuccess) return hip_fail(c, e, "fused encode+crc launch");
+    if (handled) return crc_fold(c, len, nstripes * n, crc_in, crc_out, s);
+  }
+  // two passes: encode, then the CRC of the k sources and p parities
+  hrs_status st = run_apply(c, c->g.data(), p, k, in_rows, in_stride, out_rows, out_stride, len, nstripes, s,
+                            c->kind != HRS_CODE_XOR);
+  if (st != HRS_OK) return st;
+  std::vector<const uint8_t*> rows(n);
+  std::vector<size_t> strides(n);
+  for (int i = 0; i < k; ++i) {
+    rows[i] = in_rows[i];
+    strides[i] = in_stride;
+  }
+  for (int o = 0; o < p; ++o) {
+    rows[k + o] = out_rows[o];
+    strides[k + o] = out_stride;
+  }
+  return run_crc(c, rows.data(), strides.data(), n, len, nstripes, crc_in, crc_out, s);
+}
 
 const char* hrs_version(void) { return "hrs 0.1.0 (gfx950)"; }
 

@@ -26,28 +26,12 @@
 #include <cstdint>
 #include <cstdlib>
 
-#include "hrs_crc.hpp"
+#include "hrs_device.hpp"
 
 namespace hrs {
 namespace {
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t wave_id() {
-  return __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6));
-}
-
-// Z(c) from a 4 x 256 table image in LDS.
-__device__ __forceinline__ uint32_t zmul(const uint32_t* z, uint32_t c) {
-  return z[c & 0xFFu] ^ z[256 + ((c >> 8) & 0xFFu)] ^ z[512 + ((c >> 16) & 0xFFu)] ^ z[768 + (c >> 24)];
-}
-
-// One slicing-by-4 step on this lane's table copy (entry e at e * kCrcRep).
-__device__ __forceinline__ uint32_t slice4(const uint32_t* s, uint32_t x) {
-  constexpr int R = kCrcRep;
-  return s[(3 * 256 + (x & 0xFFu)) * R] ^ s[(2 * 256 + ((x >> 8) & 0xFFu)) * R] ^
-         s[(1 * 256 + ((x >> 16) & 0xFFu)) * R] ^ s[(0 * 256 + (x >> 24)) * R];
-}
+// zmul / slice4 / lane_tree: hrs_device.hpp
 
 template <bool ALIGNED>
 __global__ void __launch_bounds__(kCrcBlockThreads) crc_window_kernel(const CrcWinArgs a) {
@@ -55,18 +39,18 @@ __global__ void __launch_bounds__(kCrcBlockThreads) crc_window_kernel(const CrcW
   for (int i = threadIdx.x; i < kCrcLdsWordsA; i += blockDim.x) lds[i] = a.tables[i];
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const uint32_t* slices = lds + (lane & (kCrcRep - 1));
+  const SliceTab slices = slice_tab(lane);
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
   const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
   const uint64_t ntasks = a.nstripes * a.nrows * wpr;
   const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-  for (uint64_t t = wave_id(); t < ntasks; t += nwaves) {
+  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
     const uint64_t sr = t / wpr;
     const uint64_t w = t - sr * wpr;
     const uint64_t stripe = sr / a.nrows;
     const int row = static_cast<int>(sr - stripe * a.nrows);
-    const uint8_t* base = a.rows[row] + stripe * a.stride;
+    const uint8_t* base = a.rows[row] + stripe * a.stride[row];
     // the window covers [end - kCrcWindow, end); bytes below lo read as zero
     const bool full = w < a.nwin;
     const int64_t end = full ? static_cast<int64_t>((w + 1) * kCrcWindow) : static_cast<int64_t>(a.len);
@@ -108,11 +92,7 @@ __global__ void __launch_bounds__(kCrcBlockThreads) crc_window_kernel(const CrcW
 #pragma unroll
       for (int q = 0; q < kCrcGroup; ++q) c = (g + q == 0) ? ch[q] : (zmul(zchunk, c) ^ ch[q]);
     }
-#pragma unroll
-    for (int lvl = 0; lvl < 6; ++lvl) {
-      const uint32_t o = __shfl_down(c, 1 << lvl, 64);
-      c = zmul(tree + lvl * 1024, c) ^ o;
-    }
+    c = lane_tree(tree, c);
     if (lane == 0) a.raw[(stripe * a.nrows_total + a.row0 + row) * wpr + w] = c;
   }
 }
@@ -129,18 +109,14 @@ __global__ void __launch_bounds__(256) crc_fold_kernel(const CrcFoldArgs a) {
   const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
   const uint64_t pad = static_cast<uint64_t>(a.G) * 64 - a.nwin;
   const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-  for (uint64_t sr = wave_id(); sr < a.nsr; sr += nwaves) {
+  for (uint64_t sr = wave_id_in_grid(); sr < a.nsr; sr += nwaves) {
     const uint32_t* raw = a.raw + sr * wpr;
     uint32_t c = 0;
     for (int g = 0; g < a.G; ++g) {
       const int64_t w = static_cast<int64_t>(lane) * a.G + g - static_cast<int64_t>(pad);
       if (w >= 0) c = zmul(zw, c) ^ raw[w];
     }
-#pragma unroll
-    for (int lvl = 0; lvl < 6; ++lvl) {
-      const uint32_t o = __shfl_down(c, 1 << lvl, 64);
-      c = zmul(ztree + lvl * 1024, c) ^ o;
-    }
+    c = lane_tree(ztree, c);
     if (lane == 0) {
       if (a.tail) c = zmul(ztail, c) ^ raw[a.nwin];
       const uint32_t state = (a.crc_in ? a.crc_in[sr] : 0u) ^ 0xFFFFFFFFu;

@@ -10,6 +10,8 @@ namespace hrs {
 
 constexpr int kCrcWindow = static_cast<int>(crc::kWindowBytes);  // bytes per wave task (32 KiB)
 constexpr int kCrcRep = 32;          // slicing tables replicated: lane l reads copy l % 32 (its own bank)
+// slicing image word of (table j, entry e, copy c); layout: hrs_device.hpp slice4
+constexpr int crc_slice_word(int j, int e, int c) { return (j >> 1) * 16384 + e * 64 + (j & 1) * 32 + c; }
 constexpr int kCrcGroup = 8;         // chunks loaded and chained together (ILP)
 constexpr int kCrcBlockThreads = 1024;  // 16 waves share one table image per CU
 constexpr int kCrcMaxRows = 32;      // rows per window launch
@@ -24,7 +26,7 @@ struct CrcWinArgs {
   int row0;         // index of rows[0] among all rows of the call
   int nrows_total;  // rows of the call (raw layout [stripe][row][window])
   int pad_;
-  uint64_t stride;  // bytes between stripes
+  uint64_t stride[kCrcMaxRows];  // bytes between stripes, per row
   uint64_t len;
   uint64_t nwin;    // full windows per row
   uint64_t tail;    // len - nwin * kCrcWindow
@@ -47,5 +49,28 @@ struct CrcFoldArgs {
 
 hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStream_t s);
 hipError_t launch_crc_fold(const CrcFoldArgs& a, int cus, hipStream_t s);
+
+// Fused encode + CRC-32 (hrs_fused.hip): one wave per (stripe, 32 KiB
+// window) encodes the window's 16 sub-windows of 2 KiB and keeps the raw CRC
+// of every data and parity row of the window, in the window kernel's exact
+// decomposition, so crc_fold_kernel finishes them. Raw layout
+// [stripe][row][window], rows = [data 0..k-1, parity 0..p-1].
+constexpr int kFusedMaxK = 16;
+constexpr int kFusedMaxP = 4;
+struct EncodeCrcArgs {
+  const uint8_t* in[kFusedMaxK];
+  uint8_t* out[kFusedMaxP];
+  uint64_t in_stride;
+  uint64_t out_stride;
+  uint64_t nwin;      // 32 KiB windows per row (len / kCrcWindow, len a multiple)
+  uint64_t nstripes;
+  uint32_t* raw;
+  const uint32_t* tables;  // kCrcLdsWordsA words (device)
+};
+
+// family: kStaticRs / kStaticCauchy (hrs_internal.hpp). *handled = false when
+// (family, k, p) has no fused kernel (the caller runs encode, then CRC).
+hipError_t launch_encode_crc(int family, int k, int p, const EncodeCrcArgs& a, int cus, hipStream_t s,
+                             bool* handled);
 
 }  // namespace hrs

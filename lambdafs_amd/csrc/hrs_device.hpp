@@ -1,0 +1,221 @@
+// Device helpers shared by the gfx950 kernels: the bit-slice transform and
+// GF(2^8) plane arithmetic (hrs_kernels.hip, hrs_fused.hip), the 2 KiB window
+// row loads/stores, and the CRC-32 table steps (hrs_crc.hip, hrs_fused.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gf256.hpp"
+#include "hrs_crc.hpp"
+#include "hrs_internal.hpp"
+
+namespace hrs {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Bitwise select m ? x : y in one VALU op (v_bitop3_b32, truth table 0xCA).
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
+  return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
+}
+
+// One delta-swap stage between two words: the bits of `a` at positions
+// (M << SH) trade places with the bits of `b` at positions M. Two shifts +
+// two selects = 4 VALU ops.
+template <int SH, uint32_t M>
+__device__ __forceinline__ void xchg(uint32_t& a, uint32_t& b) {
+  const uint32_t na = bsel(M << SH, b << SH, a);
+  const uint32_t nb = bsel(M, a >> SH, b);
+  a = na;
+  b = nb;
+}
+
+// Swap the 3 word-index bits with the 3 bit-in-byte bits of 8 words. Word w,
+// byte j, bit i  <->  word i, byte j, bit w. Afterwards w[i] holds bit i of
+// all 32 bytes (a bit-plane). Involution: applying it twice is the identity.
+__device__ __forceinline__ void bitslice(uint32_t (&w)[8]) {
+  xchg<1, 0x55555555u>(w[0], w[1]);
+  xchg<1, 0x55555555u>(w[2], w[3]);
+  xchg<1, 0x55555555u>(w[4], w[5]);
+  xchg<1, 0x55555555u>(w[6], w[7]);
+  xchg<2, 0x33333333u>(w[0], w[2]);
+  xchg<2, 0x33333333u>(w[1], w[3]);
+  xchg<2, 0x33333333u>(w[4], w[6]);
+  xchg<2, 0x33333333u>(w[5], w[7]);
+  xchg<4, 0x0F0F0F0Fu>(w[0], w[4]);
+  xchg<4, 0x0F0F0F0Fu>(w[1], w[5]);
+  xchg<4, 0x0F0F0F0Fu>(w[2], w[6]);
+  xchg<4, 0x0F0F0F0Fu>(w[3], w[7]);
+}
+
+// Multiply 32 sliced bytes by alpha = 2 modulo 0x11D (x^8 = x^4+x^3+x^2+1).
+__device__ __forceinline__ void xtime(uint32_t (&p)[8]) {
+  const uint32_t hi = p[7];
+  p[7] = p[6];
+  p[6] = p[5];
+  p[5] = p[4];
+  p[4] = p[3] ^ hi;
+  p[3] = p[2] ^ hi;
+  p[2] = p[1] ^ hi;
+  p[1] = p[0];
+  p[0] = hi;
+}
+
+// Lane `lane` of the wave owns bytes [lane*16, +16) and [1024 + lane*16, +16)
+// of the 2 KiB window at `p`. Only whole windows reach these kernels; the
+// row tail (len % 2 KiB) goes to the byte-granular kernel. Every byte is
+// touched once, so loads and stores are nontemporal (streaming; measured
+// +4% over default-policy accesses, tools/kernel_lab.hip).
+__device__ __forceinline__ void load_row(const uint8_t* p, int lane, uint32_t (&w)[8]) {
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + lane * 16));
+  const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 + lane * 16));
+  w[0] = x[0]; w[1] = x[1]; w[2] = x[2]; w[3] = x[3];
+  w[4] = y[0]; w[5] = y[1]; w[6] = y[2]; w[7] = y[3];
+}
+
+__device__ __forceinline__ void store_row(uint8_t* p, int lane, const uint32_t (&w)[8]) {
+  const u32x4 x = {w[0], w[1], w[2], w[3]};
+  const u32x4 y = {w[4], w[5], w[6], w[7]};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p + lane * 16));
+  __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(p + 1024 + lane * 16));
+}
+
+__device__ __forceinline__ uint32_t wave_id_in_grid() {
+  return __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+}
+
+// mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of
+// parity row o (gf::row_mask of G[o][r]). Evaluated by the compiler.
+// MATRIX is gf::EncodeMatrix<K,P> (hops RS) or gf::CauchyMatrix<K,P> (nrs).
+template <int K, int P, class MATRIX>
+struct StaticPlan {
+  uint8_t mask[P][K][8];
+  constexpr StaticPlan() : mask{} {
+    const MATRIX g;
+    for (int o = 0; o < P; ++o)
+      for (int r = 0; r < K; ++r)
+        for (int q = 0; q < 8; ++q) mask[o][r][q] = gf::row_mask(g.m[o][r], q);
+  }
+};
+
+// Accumulates the bit-sliced data row r of a window into the sliced parity
+// planes: acc[o][q] ^= XOR of the planes plan.mask[o][r][q] selects, two
+// planes per v_bitop3; an odd plane waits in pend for the next row. `has` is
+// compile-time after unrolling.
+template <int K, int P, class MATRIX>
+__device__ __forceinline__ void encode_row_acc(int r, const uint32_t (&w)[8], uint32_t (&acc)[P][8],
+                                               uint32_t (&pend)[P][8], bool (&has)[P][8]) {
+  constexpr StaticPlan<K, P, MATRIX> plan{};
+#pragma unroll
+  for (int o = 0; o < P; ++o)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if ((plan.mask[o][r][q] >> i) & 1) {
+          if (has[o][q]) {
+            acc[o][q] = xor3(acc[o][q], pend[o][q], w[i]);
+            has[o][q] = false;
+          } else {
+            pend[o][q] = w[i];
+            has[o][q] = true;
+          }
+        }
+      }
+    }
+}
+
+// ------------------------------------------------------------ CRC-32 steps
+
+// Z(c) from a 4 x 256 table image in LDS.
+__device__ __forceinline__ uint32_t zmul(const uint32_t* z, uint32_t c) {
+  return z[c & 0xFFu] ^ z[256 + ((c >> 8) & 0xFFu)] ^ z[512 + ((c >> 16) & 0xFFu)] ^ z[768 + (c >> 24)];
+}
+
+// Slicing-by-4 tables in LDS, replicated kCrcRep = 32 times so lane l reads
+// copy l % 32: ds_read_b32 banks are (address / 4) mod 32 per 32-lane group,
+// so every data lookup is conflict-free. Layout: two 64 KiB regions; entry e
+// of table j, copy c at LDS byte (j >> 1) * 65536 + 256 e + 128 (j & 1) + 4 c.
+// Then one v_perm_b32 builds a lookup address from a data byte and the lane's
+// copy word (byte 0 = 4 c, byte 1 = the data byte, byte 2 = region), instead
+// of an extract + shift-add. The image must start at LDS address 0 (kernels
+// that use it have no static LDS; the CRC tests would fail otherwise).
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+
+struct SliceTab {
+  uint32_t lw_lo;  // 4 c           (tables 0, 1)
+  uint32_t lw_hi;  // 4 c | 0x10000 (tables 2, 3)
+};
+
+__device__ __forceinline__ SliceTab slice_tab(int lane) {
+  const uint32_t c4 = static_cast<uint32_t>(lane & (kCrcRep - 1)) * 4u;
+  return SliceTab{c4, c4 | 0x10000u};
+}
+
+__device__ __forceinline__ uint32_t lds_at(uint32_t byte_addr) {
+  return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(byte_addr));
+}
+
+// One slicing-by-4 step: T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].
+__device__ __forceinline__ uint32_t slice4(const SliceTab& t, uint32_t x) {
+  const uint32_t a3 = __builtin_amdgcn_perm(x, t.lw_hi, 0x0C020400u);  // [4c, x.b0, 1, 0]
+  const uint32_t a2 = __builtin_amdgcn_perm(x, t.lw_hi, 0x0C020500u);  // [4c, x.b1, 1, 0]
+  const uint32_t a1 = __builtin_amdgcn_perm(x, t.lw_lo, 0x0C0C0600u);  // [4c, x.b2, 0, 0]
+  const uint32_t a0 = __builtin_amdgcn_perm(x, t.lw_lo, 0x0C0C0700u);  // [4c, x.b3, 0, 0]
+  return xor3(lds_at(a3 + 128u), lds_at(a2), lds_at(a1 + 128u)) ^ lds_at(a0);
+}
+
+// Raw CRC of one 16-byte piece (4 little-endian words).
+__device__ __forceinline__ uint32_t piece_crc(const SliceTab& s, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  uint32_t c = slice4(s, w0);
+  c = slice4(s, c ^ w1);
+  c = slice4(s, c ^ w2);
+  return slice4(s, c ^ w3);
+}
+
+// Raw CRCs of the lane's two pieces of M rows (row m's words x[m][0..3] and
+// x[m][4..7]), 2M chains advanced in lockstep so each step issues 8M
+// independent LDS lookups before waiting on any (one chain at a time leaves
+// the LDS latency exposed between its four dependent steps).
+template <int M>
+__device__ __forceinline__ void rows_piece_crcs(const SliceTab& t, const uint32_t (&x)[M][8], uint32_t (&c0)[M],
+                                                uint32_t (&c1)[M]) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    c0[m] = x[m][0];
+    c1[m] = x[m][4];
+  }
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      c0[m] = slice4(t, c0[m]);
+      c1[m] = slice4(t, c1[m]);
+    }
+    if (st < 3) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        c0[m] ^= x[m][st + 1];
+        c1[m] ^= x[m][st + 5];
+      }
+    }
+  }
+}
+
+// Joins the 64 lanes' raw CRCs of a window whose lane l covered the pieces at
+// 16 l + 1024 q: lane tree with Z_{16 * 2^t}; lane 0 ends with the window's.
+__device__ __forceinline__ uint32_t lane_tree(const uint32_t* tree, uint32_t c) {
+#pragma unroll
+  for (int lvl = 0; lvl < 6; ++lvl) {
+    const uint32_t o = __shfl_down(c, 1 << lvl, 64);
+    c = zmul(tree + lvl * 1024, c) ^ o;
+  }
+  return c;
+}
+
+}  // namespace hrs

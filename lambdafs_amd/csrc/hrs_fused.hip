@@ -1,0 +1,138 @@
+// gfx950 fused encode + CRC-32: the parity of every stripe and the
+// java.util.zip.CRC32 of every source and parity cell in ONE pass over HBM —
+// what Encoder.encodeStripe does per bufSize round with computeBlockChecksum
+// (sourceChecksums over readBufs before encodeBulk, parityChecksums over
+// writeBufs after it; Encoder.java:408-450). Run as two passes (encode, then
+// hrs_crc32_dev) the cells are read twice; fused, the CRC consumes the words
+// the encode already holds in registers.
+//
+// Decomposition: one wave per (stripe, 32 KiB window). The window is walked
+// as 16 sub-windows of 2 KiB — exactly the encode kernels' task (lane l holds
+// the 16-byte pieces at 16 l and 1024 + 16 l of each sub-window, i.e. chunks
+// 2i and 2i+1 of the window), so the CRC decomposition is identical to
+// crc_window_kernel's (lane l owns the piece at 1024 q + 16 l of every chunk
+// q, pieces joined in chunk order with Z_1024, lanes joined by the Z_{16*2^t}
+// tree): the raw window CRCs it writes are the ones crc_window_kernel would
+// write, and crc_fold_kernel finishes them unchanged. The slicing tables are
+// the same 32x bank-replicated LDS image (156 KiB: one block per CU).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "hrs_device.hpp"
+
+namespace hrs {
+namespace {
+
+constexpr int kSubWindows = kCrcWindow / kWindowBytes;  // 16
+
+template <int K, int P, class MATRIX, int THREADS>
+__global__ void __launch_bounds__(THREADS) encode_crc_kernel(const EncodeCrcArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  for (int i = threadIdx.x; i < kCrcLdsWordsA; i += THREADS) lds[i] = a.tables[i];
+  __syncthreads();
+  constexpr int N = K + P;
+  const int lane = threadIdx.x & 63;
+  const SliceTab slices = slice_tab(lane);
+  const uint32_t* zchunk = lds + kCrcSliceWords;
+  const uint32_t* tree = zchunk + 1024;
+  const uint64_t ntasks = a.nstripes * a.nwin;
+  const uint32_t nwaves = gridDim.x * (THREADS / 64);
+  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t w = t - stripe * a.nwin;
+    const uint64_t in_base = stripe * a.in_stride + w * kCrcWindow;
+    const uint64_t out_base = stripe * a.out_stride + w * kCrcWindow;
+    uint32_t crc[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) crc[r] = 0u;  // Z(0) = 0: the first piece needs no special case
+#pragma unroll 1
+    for (int sub = 0; sub < kSubWindows; ++sub) {
+      const uint64_t off = static_cast<uint64_t>(sub) * kWindowBytes;
+      uint32_t acc[P][8];
+      uint32_t pend[P][8];
+      bool has[P][8];
+#pragma unroll
+      for (int o = 0; o < P; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          acc[o][q] = 0u;
+          pend[o][q] = 0u;
+          has[o][q] = false;
+        }
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        uint32_t x[8];
+        load_row(a.in[r] + in_base + off, lane, x);
+        const uint32_t c0 = piece_crc(slices, x[0], x[1], x[2], x[3]);  // chunk 2 sub
+        const uint32_t c1 = piece_crc(slices, x[4], x[5], x[6], x[7]);  // chunk 2 sub + 1
+        crc[r] = zmul(zchunk, zmul(zchunk, crc[r]) ^ c0) ^ c1;
+        bitslice(x);
+        encode_row_acc<K, P, MATRIX>(r, x, acc, pend, has);
+      }
+#pragma unroll
+      for (int o = 0; o < P; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (has[o][q]) acc[o][q] ^= pend[o][q];
+#pragma unroll
+      for (int o = 0; o < P; ++o) {
+        bitslice(acc[o]);
+        store_row(a.out[o] + out_base + off, lane, acc[o]);
+      }
+      uint32_t p0[P], p1[P];
+      rows_piece_crcs<P>(slices, acc, p0, p1);
+#pragma unroll
+      for (int o = 0; o < P; ++o) crc[K + o] = zmul(zchunk, zmul(zchunk, crc[K + o]) ^ p0[o]) ^ p1[o];
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const uint32_t c = lane_tree(tree, crc[r]);
+      if (lane == 0) a.raw[(stripe * N + r) * a.nwin + w] = c;
+    }
+  }
+}
+
+// One 1024-thread block per CU (16 waves share the 156 KiB table image; the
+// kernel is VALU-bound, so every wave slot counts): 3.3-3.5 ms for 1,024
+// RS(10,4) 1 MiB stripes vs 4.2-4.3 ms with 512 threads, and prefetching
+// the next row gained < 5% at the cost of VGPR spills (tools/bench_encode_crc.py).
+constexpr int kFusedThreads = 1024;
+
+template <int K, int P, class MATRIX>
+hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
+  const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
+  const uint64_t ntasks = a.nstripes * a.nwin;
+  const int threads = kFusedThreads;
+  auto k = encode_crc_kernel<K, P, MATRIX, kFusedThreads>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     static_cast<int>(shm));
+  if (e != hipSuccess) return e;
+  const uint64_t per_block = threads / 64;
+  uint64_t g = (ntasks + per_block - 1) / per_block;
+  if (g > static_cast<uint64_t>(cus)) g = cus;
+  if (g == 0) g = 1;
+  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_encode_crc(int family, int k, int p, const EncodeCrcArgs& a, int cus, hipStream_t s,
+                             bool* handled) {
+  *handled = true;
+  if (family == kStaticCauchy) {
+    if (k == 10 && p == 4) return launch_one<10, 4, gf::CauchyMatrix<10, 4>>(a, cus, s);
+    if (k == 6 && p == 3) return launch_one<6, 3, gf::CauchyMatrix<6, 3>>(a, cus, s);
+  } else {
+    if (k == 10 && p == 4) return launch_one<10, 4, gf::EncodeMatrix<10, 4>>(a, cus, s);
+    if (k == 6 && p == 3) return launch_one<6, 3, gf::EncodeMatrix<6, 3>>(a, cus, s);
+    if (k == 3 && p == 2) return launch_one<3, 2, gf::EncodeMatrix<3, 2>>(a, cus, s);
+    if (k == 12 && p == 4) return launch_one<12, 4, gf::EncodeMatrix<12, 4>>(a, cus, s);
+  }
+  *handled = false;
+  return hipSuccess;
+}
+
+}  // namespace hrs

@@ -25,112 +25,20 @@
 
 #include <cstdlib>
 
-#include "gf256.hpp"
-#include "hrs_internal.hpp"
+#include "hrs_device.hpp"
 
 namespace hrs {
 namespace {
 
 // ---------------------------------------------------------------- helpers
 
+// bit-slice transform, plane arithmetic and window row accesses: hrs_device.hpp
 __constant__ gf::Tables d_tables = gf::make_tables();
-
-// Three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// Bitwise select m ? x : y in one VALU op (v_bitop3_b32, truth table 0xCA).
-__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
-  return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
-}
-
-// One delta-swap stage between two words: the bits of `a` at positions
-// (M << SH) trade places with the bits of `b` at positions M. Two shifts +
-// two selects = 4 VALU ops.
-template <int SH, uint32_t M>
-__device__ __forceinline__ void xchg(uint32_t& a, uint32_t& b) {
-  const uint32_t na = bsel(M << SH, b << SH, a);
-  const uint32_t nb = bsel(M, a >> SH, b);
-  a = na;
-  b = nb;
-}
-
-// Swap the 3 word-index bits with the 3 bit-in-byte bits of 8 words. Word w,
-// byte j, bit i  <->  word i, byte j, bit w. Afterwards w[i] holds bit i of
-// all 32 bytes (a bit-plane). Involution: applying it twice is the identity.
-__device__ __forceinline__ void bitslice(uint32_t (&w)[8]) {
-  xchg<1, 0x55555555u>(w[0], w[1]);
-  xchg<1, 0x55555555u>(w[2], w[3]);
-  xchg<1, 0x55555555u>(w[4], w[5]);
-  xchg<1, 0x55555555u>(w[6], w[7]);
-  xchg<2, 0x33333333u>(w[0], w[2]);
-  xchg<2, 0x33333333u>(w[1], w[3]);
-  xchg<2, 0x33333333u>(w[4], w[6]);
-  xchg<2, 0x33333333u>(w[5], w[7]);
-  xchg<4, 0x0F0F0F0Fu>(w[0], w[4]);
-  xchg<4, 0x0F0F0F0Fu>(w[1], w[5]);
-  xchg<4, 0x0F0F0F0Fu>(w[2], w[6]);
-  xchg<4, 0x0F0F0F0Fu>(w[3], w[7]);
-}
-
-// Multiply 32 sliced bytes by alpha = 2 modulo 0x11D (x^8 = x^4+x^3+x^2+1).
-__device__ __forceinline__ void xtime(uint32_t (&p)[8]) {
-  const uint32_t hi = p[7];
-  p[7] = p[6];
-  p[6] = p[5];
-  p[5] = p[4];
-  p[4] = p[3] ^ hi;
-  p[3] = p[2] ^ hi;
-  p[2] = p[1] ^ hi;
-  p[1] = p[0];
-  p[0] = hi;
-}
-
-// Lane `lane` of the wave owns bytes [lane*16, +16) and [1024 + lane*16, +16)
-// of the 2 KiB window at `p`. Only whole windows reach these kernels; the
-// row tail (len % 2 KiB) goes to the byte-granular kernel. Every byte is
-// touched once, so loads and stores are nontemporal (streaming; measured
-// +4% over default-policy accesses, tools/kernel_lab.hip).
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void load_row(const uint8_t* p, int lane, uint32_t (&w)[8]) {
-  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + lane * 16));
-  const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 + lane * 16));
-  w[0] = x[0]; w[1] = x[1]; w[2] = x[2]; w[3] = x[3];
-  w[4] = y[0]; w[5] = y[1]; w[6] = y[2]; w[7] = y[3];
-}
-
-__device__ __forceinline__ void store_row(uint8_t* p, int lane, const uint32_t (&w)[8]) {
-  const u32x4 x = {w[0], w[1], w[2], w[3]};
-  const u32x4 y = {w[4], w[5], w[6], w[7]};
-  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p + lane * 16));
-  __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(p + 1024 + lane * 16));
-}
-
-__device__ __forceinline__ uint32_t wave_id_in_grid() {
-  return __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-}
 
 // ------------------------------------------------- static encode kernels
 
-// mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of
-// parity row o (gf::row_mask of G[o][r]). Evaluated by the compiler.
-// MATRIX is gf::EncodeMatrix<K,P> (hops RS) or gf::CauchyMatrix<K,P> (nrs).
-template <int K, int P, class MATRIX>
-struct StaticPlan {
-  uint8_t mask[P][K][8];
-  constexpr StaticPlan() : mask{} {
-    const MATRIX g;
-    for (int o = 0; o < P; ++o)
-      for (int r = 0; r < K; ++r)
-        for (int q = 0; q < 8; ++q) mask[o][r][q] = gf::row_mask(g.m[o][r], q);
-  }
-};
-
 template <int K, int P, class MATRIX>
 __device__ __forceinline__ void encode_static_body(const RowArgs& a) {
-  constexpr StaticPlan<K, P, MATRIX> plan{};
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
@@ -152,25 +60,7 @@ __device__ __forceinline__ void encode_static_body(const RowArgs& a) {
       uint32_t w[8];
       load_row(a.in[r] + stripe * a.in_stride + off, lane, w);
       bitslice(w);
-      // acc[o][q] ^= XOR of the planes plan.mask[o][r][q] selects, two
-      // planes per v_bitop3; an odd plane waits in pend for the next row.
-#pragma unroll
-      for (int o = 0; o < P; ++o)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if ((plan.mask[o][r][q] >> i) & 1) {
-              if (has[o][q]) {
-                acc[o][q] = xor3(acc[o][q], pend[o][q], w[i]);
-                has[o][q] = false;
-              } else {
-                pend[o][q] = w[i];
-                has[o][q] = true;
-              }
-            }
-          }
-        }
+      encode_row_acc<K, P, MATRIX>(r, w, acc, pend, has);
     }
 #pragma unroll
     for (int o = 0; o < P; ++o)

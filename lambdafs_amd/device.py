@@ -52,6 +52,30 @@ def encode_stripes(code, stripes):
     code._check(_lib.lib().hrs_encode_dev(code._handle(), ins, s_in, outs, s_out, L, S, _stream(stripes)))
 
 
+def encode_stripes_crc(code, stripes, crc_in=None):
+    """Encode every stripe and return the CRC-32 (java.util.zip.CRC32) of its
+    cells in one pass, as Encoder.encodeStripe keeps them with
+    computeBlockChecksum (Encoder.java:408-450): an int32 tensor [S, k + p],
+    columns [source 0..k-1, parity 0..p-1] holding the uint32 CRC bits.
+    crc_in ([S, k + p] int32, same layout) continues running CRCs across
+    successive cells (CRC32.update chaining)."""
+    torch = _lib.torch
+    k, p = code.stripeSize(), code.paritySize()
+    if stripes.dim() != 3 or stripes.shape[1] != k + p:
+        raise ValueError(f"stripes must be [S, {k + p}, L]")
+    ins, s_in, L, S = _rows([stripes[:, p + c, :] for c in range(k)])
+    outs, s_out, _, _ = _rows([stripes[:, r, :] for r in range(p)])
+    crc = torch.empty((S, k + p), dtype=torch.int32, device=stripes.device)
+    cin = None
+    if crc_in is not None:
+        if crc_in.shape != crc.shape or crc_in.dtype != torch.int32 or not crc_in.is_contiguous():
+            raise ValueError(f"crc_in must be a contiguous int32 tensor [S, {k + p}]")
+        cin = crc_in.data_ptr()
+    code._check(_lib.lib().hrs_encode_crc_dev(code._handle(), ins, s_in, outs, s_out, L, S, cin, crc.data_ptr(),
+                                              _stream(stripes)))
+    return crc
+
+
 def encode_rows(code, data_rows, parity_rows):
     """encodeBulk with explicit [S, L] row views (k data, p parity)."""
     ins, s_in, L, S = _rows(data_rows)
