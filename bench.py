@@ -251,6 +251,31 @@ def main():
         raise RuntimeError("random-location batch decode failed its round-trip check")
     del out_rand
 
+    # the Encoder's block checksums (Encoder.java:408-450) fused
+    # into the encode (hrs_encode_crc_dev) vs the two passes it replaces
+    # (encode, then hrs_crc32_dev over the 14 cells); outside the timed region
+    def med_ms(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+        return ms
+
+    cells = [stripes[:, p + c, :] for c in range(k)] + [stripes[:, r, :] for r in range(p)]
+    crc_fused = device.encode_stripes_crc(code, stripes)
+    crc_two = device.crc32_rows(code, cells)
+    if not parallel.all_ok(bool(torch.equal(crc_fused, crc_two)), dev):
+        raise RuntimeError("fused encode+CRC differs from encode then CRC")
+    reps = max(3, min(args.steps, 10))
+    fused_ms = med_ms(lambda: device.encode_stripes_crc(code, stripes), reps)
+    two_ms = med_ms(lambda: (device.encode_stripes(code, stripes), device.crc32_rows(code, cells)), reps)
+
     total_stripes = args.stripes if args.strong else S * world
     user_bytes = 2 * k * L * total_stripes * args.steps
     enc_bytes = (k + p) * L * S  # algorithmic bytes per encode launch (read k, write p)
@@ -311,6 +336,14 @@ def main():
                 "algorithmic_bytes_per_launch": (k + 1) * L * S,
                 "traffic": load_traffic("batch_bitsliced_kernel<1,12>"),
                 "GiBps_user_per_gpu": round(k * L * S / GiB / (float(np.median(rand_ms)) * 1e-3), 3),
+            },
+            "encode_crc": {
+                "what": "encode + java.util.zip.CRC32 of all k+p cells (Encoder with computeBlockChecksum)",
+                "kernel": f"encode_crc_kernel<{k},{p}> + crc_fold_kernel",
+                "fused_ms": stats(fused_ms),
+                "two_pass_ms": stats(two_ms),
+                "fused_GBps_algorithmic": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9, 1),
+                "speedup_vs_two_pass": round(float(np.median(two_ms)) / float(np.median(fused_ms)), 3),
             },
             "copy_peak": peak,
             "cpu_baseline": None,
