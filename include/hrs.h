@@ -172,6 +172,26 @@ hrs_status hrs_decode(hrs_codec* codec, const uint8_t* const* read_bufs, uint8_t
 hrs_status hrs_decode3(hrs_codec* codec, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
                        const int* erased, int num_erased, size_t len);
 
+/* hrs_encode plus the block checksums Encoder.encodeStripe keeps when
+ * computeBlockChecksum is set (Encoder.java:408-450: sourceChecksums[i].update
+ * over readBufs[i], parityChecksums[i].update over writeBufs[i]):
+ * crc_out[r] = java.util.zip.CRC32 continued from crc_in[r] over input row r
+ * (r < k) or output row r - k (r >= k). crc_in / crc_out are HOST arrays of
+ * k + p uint32 (crc_in NULL = fresh CRC32 objects; crc_out may alias crc_in).
+ * Each cell is checksummed on the GPU as it passes through, in the same
+ * pipelined copy as the encode; no second host pass. */
+hrs_status hrs_encode_crc(hrs_codec* codec, const uint8_t* const* inputs, uint8_t* const* outputs,
+                          size_t len, const uint32_t* crc_in, uint32_t* crc_out);
+
+/* hrs_decode plus the CRC-32 of every repaired row (Decoder.java:222-229 and
+ * :645-655 compare it with the block checksum the NameNode holds):
+ * crc_out[i] = CRC32 continued from crc_in[i] over write_bufs[i]. HOST arrays
+ * of num_erased uint32 (crc_in NULL = fresh). */
+hrs_status hrs_decode_crc(hrs_codec* codec, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                          const int* erased, int num_erased, const int* to_read, int num_to_read,
+                          const int* not_to_read, int num_not_to_read, size_t len,
+                          const uint32_t* crc_in, uint32_t* crc_out);
+
 /* ---- device-resident batches (the MI355X hot path) ----
  * Row pointers are DEVICE pointers for stripe 0; stripe s of row r lives at
  * rows[r] + s * stride. `stream` is a hipStream_t (NULL = the null stream).
@@ -235,7 +255,9 @@ hrs_status hrs_encode_crc_dev(hrs_codec* codec, const uint8_t* const* in_rows, s
                               const uint32_t* crc_in, uint32_t* crc_out, void* stream);
 
 /* Kernel selection for tests and benchmarks: 0 = auto (default), 1 = force
- * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel. */
+ * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel,
+ * 3 = auto, except that hrs_encode_crc_dev takes the fused kernel whenever the
+ * shape allows it, however few windows the batch has. */
 hrs_status hrs_set_kernel_mode(hrs_codec* codec, int mode);
 
 #ifdef __cplusplus

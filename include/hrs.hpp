@@ -128,6 +128,33 @@ class HipCode : public ErasureCode {
           h_);
   }
 
+  // encodeBulk plus Encoder.encodeStripe's block checksums (Encoder.java:408-450):
+  // crcs (k + p: sources, then parities) are java.util.zip.CRC32 values
+  // continued over this round's cells; start them at 0 for fresh CRC32 objects.
+  void encodeBulkCrc(const std::vector<uint8_t*>& inputs, const std::vector<uint8_t*>& outputs, size_t len,
+                     std::vector<uint32_t>& crcs) {
+    if (static_cast<int>(inputs.size()) != stripeSize() || static_cast<int>(outputs.size()) != paritySize() ||
+        static_cast<int>(crcs.size()) != stripeSize() + paritySize())
+      throw std::invalid_argument("encodeBulkCrc: row or checksum counts do not match the codec");
+    std::vector<const uint8_t*> in(inputs.begin(), inputs.end());
+    check(hrs_encode_crc(h_, in.data(), outputs.data(), len, crcs.data(), crcs.data()), h_);
+  }
+
+  // decodeBulk plus the CRC32 of each repaired buffer (Decoder.java:222-229,
+  // :645-655), continued in crcs (one per erased location).
+  void decodeBulkCrc(const std::vector<uint8_t*>& readBufs, const std::vector<uint8_t*>& writeBufs, size_t len,
+                     const std::vector<int>& erased, const std::vector<int>& toRead,
+                     const std::vector<int>& notToRead, std::vector<uint32_t>& crcs) {
+    if (static_cast<int>(readBufs.size()) != stripeSize() + paritySize() || writeBufs.size() != erased.size() ||
+        crcs.size() != erased.size())
+      throw std::invalid_argument("decodeBulkCrc: row or checksum counts do not match");
+    std::vector<const uint8_t*> in(readBufs.begin(), readBufs.end());
+    check(hrs_decode_crc(h_, in.data(), writeBufs.data(), erased.data(), static_cast<int>(erased.size()),
+                         toRead.data(), static_cast<int>(toRead.size()), notToRead.data(),
+                         static_cast<int>(notToRead.size()), len, crcs.data(), crcs.data()),
+          h_);
+  }
+
   // RS-specific decodeBulk(readBufs, writeBufs, erasedLocation), ReedSolomonCode.java:168-185.
   void decodeBulk3(const std::vector<uint8_t*>& readBufs, const std::vector<uint8_t*>& writeBufs, size_t len,
                    const std::vector<int>& erased) {

@@ -33,7 +33,7 @@ EXPORTS = (
     "hrs_last_error", "hrs_version", "hrs_locations_to_read_list",
     "hrs_stripe_size", "hrs_parity_size", "hrs_symbol_size",
     "hrs_locations_to_read", "hrs_encode_matrix", "hrs_decode_matrix",
-    "hrs_encode", "hrs_decode", "hrs_decode3",
+    "hrs_encode", "hrs_decode", "hrs_decode3", "hrs_encode_crc", "hrs_decode_crc",
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
     "hrs_encode_crc_dev",
     "hrs_set_kernel_mode",
@@ -87,6 +87,8 @@ def lib():
         "hrs_encode": ([P, PP, PP, S], I),
         "hrs_decode": ([P, PP, PP, IP, I, IP, I, IP, I, S], I),
         "hrs_decode3": ([P, PP, PP, IP, I, S], I),
+        "hrs_encode_crc": ([P, PP, PP, S, P, P], I),
+        "hrs_decode_crc": ([P, PP, PP, IP, I, IP, I, IP, I, S, P, P], I),
         "hrs_encode_dev": ([P, PP, S, PP, S, S, S, P], I),
         "hrs_decode_dev": ([P, PP, S, PP, S, IP, I, IP, I, S, S, P], I),
         "hrs_decode_batch_dev": ([P, P, S, S, P, I, P, S, S, S, S, P], I),

@@ -46,6 +46,7 @@ struct hrs_codec {
   std::map<uint64_t, uint32_t*> crc_fold_tables;
   uint32_t* crc_raw = nullptr;
   size_t crc_raw_bytes = 0;
+  std::map<uint64_t, hrs::crc::Mat> crc_zmats;  // host-side Z_len, chaining chunk CRCs
   // hrs_decode_batch_dev: two slots (plans + per-stripe pattern index), each
   // a device buffer and its pinned staging; a slot is reused once the event
   // recorded after its launches has completed.
@@ -516,7 +517,7 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
   for (int o = 0; o < nout; ++o) vec_ok &= aligned16(out_rows[o]);
   const int mode = c->kernel_mode;
   if (mode == 2) vec_ok = false;
-  if (mode != 0) static_kp = false;
+  if (mode == 1 || mode == 2) static_kp = false;
 
   const uint64_t nwin = vec_ok ? len / hrs::kWindowBytes : 0;
   const uint64_t tail_off = nwin * hrs::kWindowBytes;
@@ -673,15 +674,45 @@ hrs_status host_slot(hrs_codec* c, int i, size_t bytes) {
   return HRS_OK;
 }
 
+size_t crc_raw_bytes_for(size_t len, size_t nstripes, int nrows);
+hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strides, int nrows, size_t len,
+                   size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw);
+hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
+                           size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
+                           hipStream_t s, uint32_t* raw);
+
+// Block checksums carried through a host-buffer call (Encoder.java:408-450,
+// Decoder.java:222-229 / :645-655): kCrcEncode = CRC-32 of the k inputs then
+// the p outputs (the encode matrix is c->g), kCrcOutputs = of the nout outputs.
+// Each chunk's CRCs come back with its outputs and are chained on the host,
+// crc = Z_len(crc) ^ crc_chunk (zlib crc32_combine), starting from `in`
+// (NULL = fresh CRC32 objects).
+enum HostCrcMode { kCrcNone = 0, kCrcEncode = 1, kCrcOutputs = 2 };
+struct HostCrc {
+  int mode = kCrcNone;
+  const uint32_t* in = nullptr;
+  uint32_t* out = nullptr;
+};
+
+const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
+  auto it = c->crc_zmats.find(len);
+  if (it == c->crc_zmats.end()) it = c->crc_zmats.emplace(len, hrs::crc::zeros(len)).first;
+  return it->second;
+}
+
 hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
-                      uint8_t* const* out_rows, size_t len, bool static_kp) {
+                      uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc = HostCrc()) {
+  const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
+  if (ncrc > 0) {  // the running values; an empty call leaves them as they are
+    for (int r = 0; r < ncrc; ++r) crc.out[r] = crc.in ? crc.in[r] : 0u;
+  }
   if (len == 0 || nout == 0) return HRS_OK;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   std::vector<int> slot_of(nin, -1);  // staging row of each live input
   int nlive = 0;
   for (int i = 0; i < nin; ++i) {
-    bool any = false;
+    bool any = crc.mode == kCrcEncode;  // every source is checksummed
     for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
     if (!any) continue;
     if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
@@ -692,7 +723,11 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   const size_t chunk = std::min(len, host_chunk_bytes());
   const size_t pitch = pitch_for(chunk);
   const size_t nchunks = (len + chunk - 1) / chunk;
-  const size_t need = pitch * static_cast<size_t>(nlive + nout);
+  // slot layout: nlive + nout rows of `pitch`, then (CRC only) the chunk's
+  // ncrc CRC words, then the raw window-CRC scratch (device side only)
+  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
+  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
+  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(chunk, 1, ncrc) : crc_off;
   for (int i = 0; i < 2; ++i) {
     hrs_status st = host_slot(c, i, need);
     if (st != HRS_OK) return st;
@@ -709,6 +744,11 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     for (int o = 0; o < nout; ++o)
       jobs.push_back({out_rows[o] + pend_off[sl], c->host[sl].pin + pitch * (nlive + o), pend_len[sl]});
     pool.run(jobs);
+    if (ncrc) {  // chunks finish in order: chain this one onto the running values
+      const uint32_t* part = reinterpret_cast<const uint32_t*>(c->host[sl].pin + crc_off);
+      const hrs::crc::Mat& z = crc_zmat(c, pend_len[sl]);
+      for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[r];
+    }
     pending[sl] = false;
     return HRS_OK;
   };
@@ -730,10 +770,21 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     }
     for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? h.dev + pitch * slot_of[i] : nullptr;
     for (int o = 0; o < nout; ++o) dout[o] = h.dev + pitch * (nlive + o);
-    st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
+    uint32_t* dcrc = reinterpret_cast<uint32_t*>(h.dev + crc_off);
+    uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
+    if (crc.mode == kCrcEncode)
+      st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+    else
+      st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
     if (st != HRS_OK) return st;
-    hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, pitch * (nout - 1) + lj,
-                                  hipMemcpyDeviceToHost, h.stream);
+    if (crc.mode == kCrcOutputs) {
+      std::vector<size_t> strides(nout, 0);
+      st = run_crc(c, dout.data(), strides.data(), nout, lj, 1, nullptr, dcrc, h.stream, draw);
+      if (st != HRS_OK) return st;
+    }
+    // outputs (and the chunk CRCs right behind them) back to the staging
+    const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + lj;
+    hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost, h.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
     e = hipEventRecord(h.done, h.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
@@ -837,12 +888,13 @@ hrs_status crc_scratch(hrs_codec* c, size_t bytes, hipStream_t s) {
 }
 
 // Folds the raw window CRCs of nsr (stripe, row) pairs into CRC32 values.
-hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s) {
+hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s,
+                    uint32_t* raw) {
   const uint32_t* fold = nullptr;
   hrs_status st = crc_fold_tables(c, len, &fold);
   if (st != HRS_OK) return st;
   hrs::CrcFoldArgs f{};
-  f.raw = c->crc_raw;
+  f.raw = raw;
   f.nwin = len / hrs::kCrcWindow;
   f.tail = len % hrs::kCrcWindow;
   f.nsr = nsr;
@@ -855,16 +907,22 @@ hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_
   return HRS_OK;
 }
 
+// Bytes of raw window-CRC scratch a CRC pass over nrows rows of nstripes
+// stripes needs (one word per 32 KiB window, the tail window included).
+size_t crc_raw_bytes_for(size_t len, size_t nstripes, int nrows) {
+  const uint64_t wpr = len / hrs::kCrcWindow + (len % hrs::kCrcWindow ? 1 : 0);
+  return std::max<size_t>(4, nstripes * static_cast<size_t>(nrows) * wpr * 4);
+}
+
 // CRC-32 of nrows rows per stripe, row r at rows[r] + stripe * strides[r]:
-// window pass + fold. crc_out[s * nrows + r].
+// window pass + fold, raw window CRCs in `raw` (crc_raw_bytes_for bytes).
+// crc_out[s * nrows + r].
 hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strides, int nrows, size_t len,
-                   size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s) {
+                   size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw) {
   hrs_status st = crc_window_tables(c);
   if (st != HRS_OK) return st;
   const uint64_t nwin = len / hrs::kCrcWindow, tail = len % hrs::kCrcWindow;
   const uint64_t wpr = nwin + (tail ? 1 : 0);
-  st = crc_scratch(c, nstripes * nrows * wpr * 4, s);
-  if (st != HRS_OK) return st;
   const int cus = hrs::device_cu_count();
   bool aligned = true;
   for (int r = 0; r < nrows; ++r) aligned &= aligned16(rows[r]) && strides[r] % 16 == 0;
@@ -882,13 +940,68 @@ hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strid
       a.nwin = nwin;
       a.tail = tail;
       a.nstripes = nstripes;
-      a.raw = c->crc_raw;
+      a.raw = raw;
       a.tables = c->crc_tables_a;
       hipError_t e = hrs::launch_crc_windows(a, aligned, cus, s);
       if (e != hipSuccess) return hip_fail(c, e, "crc window launch");
     }
   }
-  return crc_fold(c, len, nstripes * nrows, crc_in, crc_out, s);
+  return crc_fold(c, len, nstripes * nrows, crc_in, crc_out, s, raw);
+}
+
+// Encode + CRC-32 of the k sources and p parities (hrs_encode_crc_dev's
+// semantics) with raw window CRCs in `raw` (crc_raw_bytes_for(len, nstripes, n)).
+hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
+                           size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
+                           hipStream_t s, uint32_t* raw) {
+  const int k = c->k, p = c->p, n = c->n;
+  // one pass: a static (k, p) of rs / nrs, whole 32 KiB windows, 16-byte aligned rows
+  bool fused = (c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS) && (c->kernel_mode == 0 || c->kernel_mode == 3) &&
+               len > 0 &&
+               len % hrs::kCrcWindow == 0 && k <= hrs::kFusedMaxK && p <= hrs::kFusedMaxP &&
+               in_stride % 16 == 0 && out_stride % 16 == 0;
+  // The fused kernel runs one wave per (stripe, 32 KiB window), each wave
+  // serial over its k + p rows (~340 us per wave at RS(10,4)). Below ~8
+  // windows per CU that latency is the whole launch and the two bandwidth-
+  // bound passes finish first (a 512 KiB host-path chunk: 16 windows, 340 us
+  // fused vs ~40 us encode + CRC; profiles/r01/host_crc).
+  if (c->kernel_mode != 3)  // 3: take the fused kernel whenever the shape allows (tests)
+    fused &= nstripes * (len / hrs::kCrcWindow) >= 8ull * static_cast<uint64_t>(hrs::device_cu_count());
+  for (int i = 0; i < k && fused; ++i) fused &= aligned16(in_rows[i]);
+  for (int o = 0; o < p && fused; ++o) fused &= aligned16(out_rows[o]);
+  if (fused) {
+    hrs_status st = crc_window_tables(c);
+    if (st != HRS_OK) return st;
+    hrs::EncodeCrcArgs a{};
+    for (int i = 0; i < k; ++i) a.in[i] = in_rows[i];
+    for (int o = 0; o < p; ++o) a.out[o] = out_rows[o];
+    a.in_stride = in_stride;
+    a.out_stride = out_stride;
+    a.nwin = len / hrs::kCrcWindow;
+    a.nstripes = nstripes;
+    a.raw = raw;
+    a.tables = c->crc_tables_a;
+    bool handled = false;
+    const int family = c->kind == HRS_CODE_NRS ? hrs::kStaticCauchy : hrs::kStaticRs;
+    hipError_t e = hrs::launch_encode_crc(family, k, p, a, hrs::device_cu_count(), s, &handled);
+    if (e != hipSuccess) return hip_fail(c, e, "fused encode+crc launch");
+    if (handled) return crc_fold(c, len, nstripes * n, crc_in, crc_out, s, raw);
+  }
+  // two passes: encode, then the CRC of the k sources and p parities
+  hrs_status st = run_apply(c, c->g.data(), p, k, in_rows, in_stride, out_rows, out_stride, len, nstripes, s,
+                            c->kind != HRS_CODE_XOR);
+  if (st != HRS_OK) return st;
+  std::vector<const uint8_t*> rows(n);
+  std::vector<size_t> strides(n);
+  for (int i = 0; i < k; ++i) {
+    rows[i] = in_rows[i];
+    strides[i] = in_stride;
+  }
+  for (int o = 0; o < p; ++o) {
+    rows[k + o] = out_rows[o];
+    strides[k + o] = out_stride;
+  }
+  return run_crc(c, rows.data(), strides.data(), n, len, nstripes, crc_in, crc_out, s, raw);
 }
 
 }  // namespace
@@ -905,7 +1018,10 @@ hrs_status hrs_crc32_dev(hrs_codec* c, const uint8_t* const* rows, int nrows, si
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   std::vector<size_t> strides(nrows, stride);
-  return run_crc(c, rows, strides.data(), nrows, len, nstripes, crc_in, crc_out, static_cast<hipStream_t>(stream));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hrs_status st = crc_scratch(c, crc_raw_bytes_for(len, nstripes, nrows), s);
+  if (st != HRS_OK) return st;
+  return run_crc(c, rows, strides.data(), nrows, len, nstripes, crc_in, crc_out, s, c->crc_raw);
 }
 
 hrs_status hrs_encode_crc_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
@@ -913,57 +1029,17 @@ hrs_status hrs_encode_crc_dev(hrs_codec* c, const uint8_t* const* in_rows, size_
                               uint32_t* crc_out, void* stream) {
   if (!c) return HRS_EINVAL;
   if (!in_rows || !out_rows || !crc_out) return fail(c, HRS_EINVAL, "row or crc arrays are NULL");
-  const int k = c->k, p = c->p, n = c->n;
-  for (int i = 0; i < k; ++i)
+  for (int i = 0; i < c->k; ++i)
     if (!in_rows[i] && len) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
-  for (int o = 0; o < p; ++o)
+  for (int o = 0; o < c->p; ++o)
     if (!out_rows[o] && len) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
   if (nstripes == 0) return HRS_OK;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // one pass: a static (k, p) of rs / nrs, whole 32 KiB windows, 16-byte aligned rows
-  bool fused = (c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS) && c->kernel_mode == 0 && len > 0 &&
-               len % hrs::kCrcWindow == 0 && k <= hrs::kFusedMaxK && p <= hrs::kFusedMaxP &&
-               in_stride % 16 == 0 && out_stride % 16 == 0;
-  for (int i = 0; i < k && fused; ++i) fused &= aligned16(in_rows[i]);
-  for (int o = 0; o < p && fused; ++o) fused &= aligned16(out_rows[o]);
-  if (fused) {
-    hrs_status st = crc_window_tables(c);
-    if (st != HRS_OK) return st;
-    const uint64_t nwin = len / hrs::kCrcWindow;
-    st = crc_scratch(c, nstripes * n * nwin * 4, s);
-    if (st != HRS_OK) return st;
-    hrs::EncodeCrcArgs a{};
-    for (int i = 0; i < k; ++i) a.in[i] = in_rows[i];
-    for (int o = 0; o < p; ++o) a.out[o] = out_rows[o];
-    a.in_stride = in_stride;
-    a.out_stride = out_stride;
-    a.nwin = nwin;
-    a.nstripes = nstripes;
-    a.raw = c->crc_raw;
-    a.tables = c->crc_tables_a;
-    bool handled = false;
-    const int family = c->kind == HRS_CODE_NRS ? hrs::kStaticCauchy : hrs::kStaticRs;
-    hipError_t e = hrs::launch_encode_crc(family, k, p, a, hrs::device_cu_count(), s, &handled);
-    if (e != hipSuccess) return hip_fail(c, e, "fused encode+crc launch");
-    if (handled) return crc_fold(c, len, nstripes * n, crc_in, crc_out, s);
-  }
-  // two passes: encode, then the CRC of the k sources and p parities
-  hrs_status st = run_apply(c, c->g.data(), p, k, in_rows, in_stride, out_rows, out_stride, len, nstripes, s,
-                            c->kind != HRS_CODE_XOR);
+  hrs_status st = crc_scratch(c, crc_raw_bytes_for(len, nstripes, c->n), s);
   if (st != HRS_OK) return st;
-  std::vector<const uint8_t*> rows(n);
-  std::vector<size_t> strides(n);
-  for (int i = 0; i < k; ++i) {
-    rows[i] = in_rows[i];
-    strides[i] = in_stride;
-  }
-  for (int o = 0; o < p; ++o) {
-    rows[k + o] = out_rows[o];
-    strides[k + o] = out_stride;
-  }
-  return run_crc(c, rows.data(), strides.data(), n, len, nstripes, crc_in, crc_out, s);
+  return encode_crc_impl(c, in_rows, in_stride, out_rows, out_stride, len, nstripes, crc_in, crc_out, s, c->crc_raw);
 }
 
 const char* hrs_version(void) { return "hrs 0.1.0 (gfx950)"; }
@@ -1102,7 +1178,7 @@ int hrs_parity_size(const hrs_codec* c) { return c ? c->p : -1; }
 int hrs_symbol_size(const hrs_codec* c) { return c ? 8 : -1; }  // log2(256), ReedSolomonCode.java:223-226
 
 hrs_status hrs_set_kernel_mode(hrs_codec* c, int mode) {
-  if (!c || mode < 0 || mode > 2) return HRS_EINVAL;
+  if (!c || mode < 0 || mode > 3) return HRS_EINVAL;
   c->kernel_mode = mode;
   return HRS_OK;
 }
@@ -1183,6 +1259,40 @@ hrs_status hrs_encode(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const
   if (!c) return HRS_EINVAL;
   if (!inputs || !outputs) return fail(c, HRS_EINVAL, "inputs/outputs is NULL");
   return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind != HRS_CODE_XOR);
+}
+
+hrs_status hrs_encode_crc(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len,
+                          const uint32_t* crc_in, uint32_t* crc_out) {
+  if (!c) return HRS_EINVAL;
+  if (!inputs || !outputs || !crc_out) return fail(c, HRS_EINVAL, "inputs/outputs/crc_out is NULL");
+  HostCrc crc;
+  crc.mode = kCrcEncode;
+  crc.in = crc_in;
+  crc.out = crc_out;
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind != HRS_CODE_XOR, crc);
+}
+
+hrs_status hrs_decode_crc(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                          const int* erased, int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len,
+                          const uint32_t* crc_in, uint32_t* crc_out) {
+  if (!c) return HRS_EINVAL;
+  (void)to_read;
+  if (!read_bufs || (ne > 0 && (!write_bufs || !erased || !crc_out)) || ne < 0 || nn < 0 || nr < 0 ||
+      (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) ||
+      (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+    return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
+  if (ne == 0) return HRS_OK;
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d, to_read, to_read ? nr : -1);
+  if (st != HRS_OK) return st;
+  HostCrc crc;
+  crc.mode = kCrcOutputs;
+  crc.in = crc_in;
+  crc.out = crc_out;
+  return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false, crc);
 }
 
 hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,

@@ -211,7 +211,8 @@ class _HipErasureCode(ErasureCode):
         return list(buf[: cnt.value])
 
     def setKernelMode(self, mode):
-        """0 auto, 1 runtime-matrix bit-sliced kernel, 2 byte-granular kernel."""
+        """0 auto, 1 runtime-matrix bit-sliced kernel, 2 byte-granular kernel,
+        3 auto but the fused encode+CRC kernel on every eligible shape."""
         self._check(_lib.lib().hrs_set_kernel_mode(self._handle(), int(mode)))
 
     # -- matrices (host)
@@ -295,6 +296,65 @@ class _HipErasureCode(ErasureCode):
             self._handle(), reads.ptrs, writes.ptrs, int_array(erasedLocations), len(erasedLocations),
             int_array(locationsToRead), len(locationsToRead), int_array(locationsNotToRead),
             len(locationsNotToRead), reads.len))
+
+    # -- bulk with block checksums (host rows: the JNI path)
+    @staticmethod
+    def _crc_arrays(crcs, n):
+        out = np.zeros(n, dtype=np.uint32)
+        if crcs is None:
+            return None, out
+        crc_in = np.ascontiguousarray(np.asarray(crcs, dtype=np.uint64).astype(np.uint32))
+        if crc_in.shape != (n,):
+            raise ValueError(f"need {n} running CRC values")
+        return crc_in, out
+
+    def encodeBulkCrc(self, inputs, outputs, crcs=None):
+        """encodeBulk plus Encoder.encodeStripe's block checksums
+        (Encoder.java:408-450): returns k + p CRC32 values, sources then
+        parities, each continued from `crcs` (CRC32.update chaining across
+        successive cells of a block; None = fresh CRC32 objects)."""
+        if len(inputs) != self._k or len(outputs) != self._p:
+            raise ValueError(f"encodeBulk needs {self._k} inputs and {self._p} outputs")
+        ins = _Rows(inputs, writable=False)
+        outs = _Rows(outputs, writable=True)
+        if ins.len != outs.len:
+            raise ValueError("input and output rows differ in length")
+        if ins.device is not None or outs.device is not None:
+            raise ValueError("encodeBulkCrc takes host rows (device rows: device.encode_crc_stripes)")
+        crc_in, crc_out = self._crc_arrays(crcs, self._k + self._p)
+        self._check(_lib.lib().hrs_encode_crc(self._handle(), ins.ptrs, outs.ptrs, ins.len,
+                                              None if crc_in is None else crc_in.ctypes.data, crc_out.ctypes.data))
+        if self.zero_inputs_after_encode:
+            for v in ins.views:
+                if v.flags["WRITEABLE"]:
+                    v[:] = 0
+        return [int(x) for x in crc_out]
+
+    def decodeBulkCrc(self, readBufs, writeBufs, erasedLocations, locationsToRead, locationsNotToRead, crcs=None):
+        """5-arg decodeBulk plus the CRC32 of every repaired buffer, the value
+        Decoder compares with the stored block checksum (Decoder.java:222-229,
+        :645-655); continued from `crcs` (None = fresh)."""
+        n = self._k + self._p
+        if len(readBufs) != n:
+            raise ValueError(f"decodeBulk needs {n} read buffers")
+        if len(writeBufs) != len(erasedLocations):
+            raise ValueError("one write buffer per erased location")
+        ntr = set(locationsNotToRead)
+        reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
+                      writable=False, allow_none=True)
+        writes = _Rows(writeBufs, writable=True)
+        if reads.device is not None:
+            raise ValueError("decodeBulkCrc takes host rows")
+        crc_in, crc_out = self._crc_arrays(crcs, len(erasedLocations))
+        if not erasedLocations:
+            return []
+        locationsToRead = locationsToRead or []
+        self._check(_lib.lib().hrs_decode_crc(
+            self._handle(), reads.ptrs, writes.ptrs, int_array(erasedLocations), len(erasedLocations),
+            int_array(locationsToRead), len(locationsToRead), int_array(locationsNotToRead),
+            len(locationsNotToRead), reads.len, None if crc_in is None else crc_in.ctypes.data,
+            crc_out.ctypes.data))
+        return [int(x) for x in crc_out]
 
     def _apply_dev(self, m, reads, writes):
         stream = _lib.torch.cuda.current_stream(reads.device).cuda_stream

@@ -10,6 +10,9 @@
 //    built as at :303-338; zeros for erased / not-to-read inputs
 //    (StripeReader.java:106-124); code.decodeBulk(...) per round (:352-353);
 //    the repaired block's CRC32 compared with the stored one (:222-229).
+//  The codec calls are the checksummed variants (encodeBulkCrc /
+//  decodeBulkCrc, hrs_encode_crc / hrs_decode_crc); the engine's running
+//  CRCs must equal zlib's over the same bytes (gpu_crc_mismatches).
 //
 // Usage: codec_harness [--host-only] [--xor | --nrs | --src=S] k p blockSize bufSize nerased seed
 // --src=S drives SimpleRegeneratingCode with S SRC parities (local groups;
@@ -124,6 +127,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < k; ++i) fill(src[i], seed * 1000 + i);
     std::vector<std::vector<uint8_t>> parity(p, std::vector<uint8_t>(block));
     std::vector<uint32_t> src_crc(k, 0), par_crc(p, 0);
+    std::vector<uint32_t> gpu_crc(n, 0);  // the engine's own checksums (hrs_encode_crc)
 
     // ---- Encoder.encodeStripe
     size_t mismatches = 0;
@@ -140,7 +144,7 @@ int main(int argc, char** argv) {
       }
       for (int r = 0; r < p; ++r) wp[r] = write_bufs[r].data();
       auto t0 = std::chrono::steady_clock::now();
-      code->encodeBulk(rp, wp, len);
+      code->encodeBulkCrc(rp, wp, len, gpu_crc);
       t_codec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       // oracle: the Java remainder on copies (it zeroes its inputs)
       std::vector<std::vector<uint8_t>> cp = read;
@@ -197,7 +201,7 @@ int main(int argc, char** argv) {
     auto stripe_row = [&](int loc) -> const uint8_t* {
       return loc < p ? parity[loc].data() : src[loc - p].data();
     };
-    std::vector<uint32_t> rep_crc(erased_arr.size(), 0);
+    std::vector<uint32_t> rep_crc(erased_arr.size(), 0), gpu_rep_crc(erased_arr.size(), 0);
     size_t rep_mismatch = 0;
     const int ne = static_cast<int>(erased_arr.size());
     // the block writeBufs[i] receives: erased_arr[i], or for nrs the i-th
@@ -225,7 +229,7 @@ int main(int argc, char** argv) {
       }
       for (int i = 0; i < ne; ++i) wp[i] = wb[i].data();
       auto t0 = std::chrono::steady_clock::now();
-      code->decodeBulk(rp, wp, len, erased_arr, to_read_arr, ntr_arr);
+      code->decodeBulkCrc(rp, wp, len, erased_arr, to_read_arr, ntr_arr, gpu_rep_crc);
       t_codec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       for (int i = 0; i < ne; ++i) {
         rep_mismatch += std::memcmp(wb[i].data(), stripe_row(expect[i]) + off, len) != 0;
@@ -257,13 +261,17 @@ int main(int argc, char** argv) {
       const uint32_t stored = loc < p ? par_crc[loc] : src_crc[loc - p];  // checksums sent to the NN
       crc_bad += stored != rep_crc[i];
     }
-    const bool ok = mismatches == 0 && rep_mismatch == 0 && crc_bad == 0;
+    size_t gpu_crc_bad = 0;  // engine checksums vs zlib over the same bytes
+    for (int i = 0; i < k; ++i) gpu_crc_bad += gpu_crc[i] != src_crc[i];
+    for (int r = 0; r < p; ++r) gpu_crc_bad += gpu_crc[k + r] != par_crc[r];
+    for (int i = 0; i < ne; ++i) gpu_crc_bad += gpu_rep_crc[i] != rep_crc[i];
+    const bool ok = mismatches == 0 && rep_mismatch == 0 && crc_bad == 0 && gpu_crc_bad == 0;
     printf("{\"code\": \"%s\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"erased\": [", use_xor ? "xor" : use_nrs ? "nrs" : use_src ? "src" : "rs",
            k, p, block, buf);
     for (int i = 0; i < ne; ++i) printf("%s%d", i ? ", " : "", erased_arr[i]);
     printf("], \"quirk\": %s, \"encode_round_mismatches\": %zu, \"repair_mismatches\": %zu, \"crc_mismatches\": %zu, "
-           "\"codec_seconds\": %.4f, \"ok\": %s}\n",
-           quirk ? "true" : "false", mismatches, rep_mismatch, crc_bad, t_codec, ok ? "true" : "false");
+           "\"gpu_crc_mismatches\": %zu, \"codec_seconds\": %.4f, \"ok\": %s}\n",
+           quirk ? "true" : "false", mismatches, rep_mismatch, crc_bad, gpu_crc_bad, t_codec, ok ? "true" : "false");
     return ok ? 0 : 1;
   } catch (const std::exception& e) {
     printf("{\"error\": \"%s\", \"ok\": false}\n", e.what());

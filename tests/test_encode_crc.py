@@ -6,9 +6,10 @@ readBufs, encodeBulk, parityChecksums over writeBufs), in one pass.
 Parity is checked against the engine's own encode (itself pinned to the
 oracle in test_gpu_parity.py) and, on sampled stripes, against the oracle
 directly; CRCs against zlib.crc32 (the JDK's CRC32 is zlib's CRC-32). Both the
-fused kernel (static shapes, 32 KiB-multiple cells) and the two-pass fallback
-(other shapes, ragged cells, unaligned rows, forced runtime kernel) are
-covered."""
+fused kernel (static shapes, 32 KiB-multiple cells; kernel mode 3 forces it
+on small batches) and the two-pass fallback (other shapes, ragged cells,
+unaligned rows, forced runtime kernel, batches of fewer than 8 windows per CU
+in auto mode) are covered."""
 import zlib
 
 import numpy as np
@@ -52,6 +53,7 @@ def _reference_parity(torch, code, st):
 def test_fused_static_shapes(cuda, cls, k, p):
     torch = cuda
     code = cls(k, p)
+    code.setKernelMode(3)  # the fused kernel even for a 10-window batch
     S, L = 5, 64 << 10
     g = torch.Generator(device="cuda")
     g.manual_seed(k * 100 + p)
@@ -70,6 +72,7 @@ def test_fused_rs104_1mib_vs_oracle(cuda):
     torch = cuda
     k, p, L, S = 10, 4, 1 << 20, 12
     code = HipReedSolomonCode(k, p)
+    code.setKernelMode(3)
     st = torch.randint(0, 256, (S, k + p, L), dtype=torch.uint8, device="cuda")
     st[0] = 0
     st[1] = 0xFF
@@ -90,6 +93,7 @@ def test_fused_chaining_like_CRC32_update(cuda):
     torch = cuda
     k, p, L, S, rounds = 10, 4, 256 << 10, 3, 4
     code = HipReedSolomonCode(k, p)
+    code.setKernelMode(3)
     cells = [torch.randint(0, 256, (S, k + p, L), dtype=torch.uint8, device="cuda") for _ in range(rounds)]
     crc = None
     for c in cells:
@@ -107,7 +111,7 @@ def test_fused_chaining_like_CRC32_update(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["ragged", "shape", "forced_runtime", "unaligned"])
+@pytest.mark.parametrize("case", ["ragged", "shape", "forced_runtime", "unaligned", "small_batch"])
 def test_two_pass_fallback(cuda, case):
     torch = cuda
     k, p, L, S = 10, 4, 96 << 10, 3

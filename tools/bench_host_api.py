@@ -1,6 +1,8 @@
 """Throughput of the synchronous host-buffer calls (the JNI path):
 ReedSolomonCode.encodeBulk / decodeBulk on pageable host rows, one call per
-1 MiB-cell stripe, exactly as Encoder.java:442 / Decoder.java:352 issue them.
+1 MiB-cell stripe, exactly as Encoder.java:442 / Decoder.java:352 issue them;
+and the checksummed variants (hrs_encode_crc / hrs_decode_crc) next to the
+host zlib CRC pass they replace (Encoder.java:434-447).
 
 Run: python tools/bench_host_api.py [--calls 40]
 """
@@ -38,6 +40,17 @@ def main():
     for _ in range(args.calls):
         code.encodeBulk(data, par)
     te = (time.perf_counter() - t0) / args.calls
+    crcs = code.encodeBulkCrc(data, par)  # warm
+    t0 = time.perf_counter()
+    for _ in range(args.calls):
+        crcs = code.encodeBulkCrc(data, par, crcs)
+    tec = (time.perf_counter() - t0) / args.calls
+    # the Java Encoder's checksum pass on the host (zlib = java.util.zip.CRC32), 1 thread
+    import zlib
+    t0 = time.perf_counter()
+    for r in data + par:
+        zlib.crc32(r)
+    tz = time.perf_counter() - t0
     stripe = par + data
     erased = [p]
     to_read = sorted(code.locationsToReadForDecode(erased))
@@ -50,6 +63,11 @@ def main():
     for _ in range(args.calls):
         code.decodeBulk(reads, out, erased, to_read, ntr)
     td = (time.perf_counter() - t0) / args.calls
+    code.decodeBulkCrc(reads, out, erased, to_read, ntr)
+    t0 = time.perf_counter()
+    for _ in range(args.calls):
+        code.decodeBulkCrc(reads, out, erased, to_read, ntr)
+    tdc = (time.perf_counter() - t0) / args.calls
     print(json.dumps({
         "path": "synchronous host-buffer calls (hrs_encode / hrs_decode), pageable rows, 1 call per stripe",
         "copy_threads": os.environ.get("HRS_HOST_THREADS", "2 (default)"),
@@ -57,7 +75,11 @@ def main():
         "encodeBulk_ms_per_call": round(te * 1e3, 3),
         "encodeBulk_GiBps_user_data": round(k * L / GiB / te, 2),
         "encodeBulk_GBps_pcie": round((k + p) * L / te / 1e9, 2),
+        "encodeBulkCrc_ms_per_call": round(tec * 1e3, 3),
+        "encodeBulkCrc_GiBps_user_data": round(k * L / GiB / tec, 2),
+        "host_zlib_crc_of_stripe_ms_1thread": round(tz * 1e3, 3),
         "decodeBulk_ms_per_call": round(td * 1e3, 3),
+        "decodeBulkCrc_ms_per_call": round(tdc * 1e3, 3),
         "decodeBulk_GiBps_user_data": round(k * L / GiB / td, 2),
     }), flush=True)
 
