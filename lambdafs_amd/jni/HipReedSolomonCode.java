@@ -52,6 +52,35 @@ public class HipReedSolomonCode extends ErasureCode {
     }
   }
 
+  /**
+   * encodeBulk plus the block checksums Encoder.encodeStripe keeps with
+   * computeBlockChecksum (Encoder.java:408-450): crcs[k + p] holds the running
+   * CRC32 values (sources, then parities; getValue() truncated to int, 0 for a
+   * fresh CRC32) and is updated in place, so the Encoder's updateChecksums and
+   * parityChecksums passes over the heap buffers go away.
+   */
+  public void encodeBulkWithChecksums(byte[][] inputs, byte[][] outputs, int[] crcs) throws IOException {
+    assert (stripeSize == inputs.length);
+    assert (paritySize == outputs.length);
+    HrsNative.encodeCrc(nativeCodec, inputs, outputs, outputs[0].length, crcs);
+    for (byte[] in : inputs) {
+      Arrays.fill(in, (byte) 0);
+    }
+  }
+
+  /**
+   * 5-arg decodeBulk plus the CRC32 of each repaired buffer, continued in
+   * crcs[erasedLocations.length] (Decoder.java:222-229, :645-655).
+   */
+  public void decodeBulkWithChecksums(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocations,
+      int[] locationsToRead, int[] locationsNotToRead, int[] crcs) throws IOException {
+    if (erasedLocations.length == 0) {
+      return;
+    }
+    HrsNative.decodeCrc(nativeCodec, readBufs, writeBufs, erasedLocations, locationsToRead,
+        locationsNotToRead, readBufs[0].length, crcs);
+  }
+
   /** Same result as ReedSolomonCode.decodeBulk 5-arg (ReedSolomonCode.java:191-211). */
   @Override
   public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocations,

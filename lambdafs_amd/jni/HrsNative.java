@@ -36,4 +36,12 @@ final class HrsNative {
 
   static native void decode3(long codec, byte[][] readBufs, byte[][] writeBufs, int[] erased, int len)
       throws IOException;
+
+  // hrs_encode_crc: crcs[k + p] (sources, then parities) continued in place
+  static native void encodeCrc(long codec, byte[][] inputs, byte[][] outputs, int len, int[] crcs)
+      throws IOException;
+
+  // hrs_decode_crc: crcs[erased.length] continued in place over writeBufs
+  static native void decodeCrc(long codec, byte[][] readBufs, byte[][] writeBufs, int[] erased, int[] toRead,
+      int[] notToRead, int len, int[] crcs) throws IOException;
 }

@@ -175,3 +175,74 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_decode3(
   unpin_rows(env, ni > 0 ? ni : 0, io, ip, JNI_ABORT);
   if (st != HRS_OK) throw_status(env, st, c);
 }
+
+/* Running checksums as a Java int[] (CRC32.getValue() & 0xFFFFFFFF):
+ * read before the rows are pinned, written back after they are released. */
+static int copy_crcs(JNIEnv* env, jintArray a, uint32_t* out, int want) {
+  if (!a || (*env)->GetArrayLength(env, a) != want || want > MAX_ROWS) return -1;
+  (*env)->GetIntArrayRegion(env, a, 0, want, (jint*)out);
+  return want;
+}
+
+/* Encoder.encodeStripe with computeBlockChecksum (Encoder.java:408-450):
+ * crcs[k + p] = sourceChecksums then parityChecksums, updated in place. */
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_encodeCrc(JNIEnv* env, jclass cls, jlong h,
+                                                                       jobjectArray inputs, jobjectArray outputs,
+                                                                       jint len, jintArray crcs) {
+  (void)cls;
+  hrs_codec* c = (hrs_codec*)(intptr_t)h;
+  uint32_t crc[MAX_ROWS];
+  int ncrc = copy_crcs(env, crcs, crc, hrs_stripe_size(c) + hrs_parity_size(c));
+  jbyteArray io[MAX_ROWS], oo[MAX_ROWS];
+  uint8_t *ip[MAX_ROWS], *op[MAX_ROWS];
+  int ni = fetch_rows(env, inputs, io, ip);
+  int no = fetch_rows(env, outputs, oo, op);
+  const int ok = ni >= 0 && no >= 0 && ncrc >= 0;
+  if (ok) {
+    pin_rows(env, ni, io, ip);
+    pin_rows(env, no, oo, op);
+  }
+  hrs_status st = ok ? hrs_encode_crc(c, (const uint8_t* const*)ip, op, (size_t)len, crc, crc) : HRS_EINVAL;
+  if (ok) {
+    unpin_rows(env, no, oo, op, 0);
+    unpin_rows(env, ni, io, ip, JNI_ABORT);
+  }
+  if (st != HRS_OK) {
+    throw_status(env, st, c);
+    return;
+  }
+  (*env)->SetIntArrayRegion(env, crcs, 0, ncrc, (const jint*)crc);
+}
+
+/* Decoder's repaired-block check (Decoder.java:222-229, :645-655):
+ * crcs[erased.length] continued over writeBufs[i], updated in place. */
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_decodeCrc(
+    JNIEnv* env, jclass cls, jlong h, jobjectArray readBufs, jobjectArray writeBufs, jintArray erased,
+    jintArray toRead, jintArray notToRead, jint len, jintArray crcs) {
+  (void)cls;
+  hrs_codec* c = (hrs_codec*)(intptr_t)h;
+  int e[MAX_ROWS], r[MAX_ROWS], ntr[MAX_ROWS];
+  int ne = copy_ints(env, erased, e), nr = copy_ints(env, toRead, r), nn = copy_ints(env, notToRead, ntr);
+  uint32_t crc[MAX_ROWS];
+  int ncrc = copy_crcs(env, crcs, crc, ne);
+  jbyteArray io[MAX_ROWS], oo[MAX_ROWS];
+  uint8_t *ip[MAX_ROWS], *op[MAX_ROWS];
+  int ni = fetch_rows(env, readBufs, io, ip);
+  int no = fetch_rows(env, writeBufs, oo, op);
+  const int ok = ni >= 0 && no >= 0 && ncrc >= 0;
+  if (ok) {
+    pin_rows(env, ni, io, ip);
+    pin_rows(env, no, oo, op);
+  }
+  hrs_status st = ok ? hrs_decode_crc(c, (const uint8_t* const*)ip, op, e, ne, r, nr, ntr, nn, (size_t)len, crc, crc)
+                     : HRS_EINVAL;
+  if (ok) {
+    unpin_rows(env, no, oo, op, 0);
+    unpin_rows(env, ni, io, ip, JNI_ABORT);
+  }
+  if (st != HRS_OK) {
+    throw_status(env, st, c);
+    return;
+  }
+  (*env)->SetIntArrayRegion(env, crcs, 0, ncrc, (const jint*)crc);
+}
