@@ -150,6 +150,17 @@ def stats(ms):
             "min": round(float(np.min(ms)), 4)}
 
 
+# The software-pipelined kernels are the default (HRS_PIPE=0: the plain ones);
+# names as rocprofv3 reports them, keys of profiles/pmc_traffic.json.
+PIPE = os.environ.get("HRS_PIPE", "1") != "0"
+DEC_KERNEL = "bitsliced_pipe_kernel<1,12>" if PIPE else "bitsliced_kernel<1,12>"
+BATCH_KERNEL = "batch_bitsliced_kernel<1,12>"
+
+
+def enc_kernel_name(k, p):
+    return f"encode_static_kernel<{k},{p}>"
+
+
 def load_traffic(kernel):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -282,7 +293,7 @@ def main():
     dec_bytes = (k + len(erased)) * L * S
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
-    kernel = f"encode_static_kernel<{k},{p}>"
+    kernel = enc_kernel_name(k, p)
     res = None
     peak = copy_peak(dev, code) if rank == 0 else None
     if rank == 0:
@@ -322,19 +333,19 @@ def main():
                 "frac_vs_copy": round(enc_gbps / peak["GBps"], 4),
             },
             "decode_roofline": {
-                "kernel": "bitsliced_kernel<1,12>", "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
+                "kernel": DEC_KERNEL, "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(dec_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(dec_ms, 4),
                 "launch_ms": stats(dec_all), "frac_vs_copy": round(dec_gbps / peak["GBps"], 4),
-                "traffic": load_traffic("bitsliced_kernel<1,12>"),
+                "traffic": load_traffic(DEC_KERNEL),
                 "algorithmic_bytes_per_launch": dec_bytes,
             },
             "random_location_decode": {
                 "what": "config 3 second run: one seeded random lost location per stripe, one batch launch",
                 "launch_ms": stats(rand_ms),
-                "kernel": "batch_bitsliced_kernel<1,12>",
+                "kernel": BATCH_KERNEL,
                 "GBps_algorithmic": round((k + 1) * L * S / (float(np.median(rand_ms)) * 1e-3) / 1e9, 1),
                 "algorithmic_bytes_per_launch": (k + 1) * L * S,
-                "traffic": load_traffic("batch_bitsliced_kernel<1,12>"),
+                "traffic": load_traffic(BATCH_KERNEL),
                 "GiBps_user_per_gpu": round(k * L * S / GiB / (float(np.median(rand_ms)) * 1e-3), 3),
             },
             "encode_crc": {

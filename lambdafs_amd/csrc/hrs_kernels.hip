@@ -169,6 +169,84 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
   }
 }
 
+// Software-pipelined form of bitsliced_kernel for narrow outputs: two
+// register sets of NINB rows, the next task's rows are loaded before the
+// current task's math, so a wave keeps a window in flight while it computes
+// (the plain kernel's loads sit idle during its ~1,000 VALU of slicing and
+// multiplying). 2*NINB*8 + 8*NOUT VGPRs: NOUT <= 2, NINB <= 12 at 2 waves/SIMD.
+template <int NOUT, int NINB>
+__device__ __forceinline__ void load_task(const RowArgs& a, uint64_t t, int nin, int lane,
+                                          uint32_t (&rows)[NINB][8]) {
+  const uint64_t stripe = t / a.nwin;
+  const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+  const uint64_t in_base = stripe * a.in_stride + off;
+#pragma unroll
+  for (int r = 0; r < NINB; ++r)
+    if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
+}
+
+template <int NOUT, int NINB>
+__device__ __forceinline__ void apply_task(const RowArgs& a, uint64_t t, int nin, int lane,
+                                           uint32_t (&rows)[NINB][8]) {
+  const uint64_t stripe = t / a.nwin;
+  const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+  uint32_t acc[NOUT][8];
+  if (a.accumulate) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      load_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+      bitslice(acc[o]);
+    }
+  } else {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < NINB; ++r) {
+    if (r < nin) {
+      bitslice(rows[r]);
+      uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
+      asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+        if (b < 7) xtime(rows[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    bitslice(acc[o]);
+    store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+  }
+}
+
+template <int NOUT, int NINB>
+__global__ void __launch_bounds__(kBlockThreads) bitsliced_pipe_kernel(const RowArgs a) {
+  static_assert(!BitLoop<NOUT, NINB>::kRolled, "pipelined kernel takes the unrolled shapes only");
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  int nin = a.nin;
+  asm volatile("" : "+s"(nin));
+  uint64_t t = wave_id_in_grid();
+  if (t >= a.ntasks) return;
+  uint32_t ra[NINB][8], rb[NINB][8];
+  load_task<NOUT, NINB>(a, t, nin, lane, ra);
+  for (;;) {  // every wave leaves once its next task index passes ntasks
+    const uint64_t t1 = t + nwaves;
+    if (t1 < a.ntasks) load_task<NOUT, NINB>(a, t1, nin, lane, rb);
+    apply_task<NOUT, NINB>(a, t, nin, lane, ra);
+    if (t1 >= a.ntasks) break;
+    const uint64_t t2 = t1 + nwaves;
+    if (t2 < a.ntasks) load_task<NOUT, NINB>(a, t2, nin, lane, ra);
+    apply_task<NOUT, NINB>(a, t1, nin, lane, rb);
+    if (t2 >= a.ntasks) break;
+    t = t2;
+  }
+}
+
 // ------------------------------------------------------------- XOR kernel
 
 // out[0] = XOR of the nin input rows (XOR code, XORCode.java:99-145; also any
@@ -363,17 +441,20 @@ int device_cus() {
 // window's rows in flight) measured fastest for both the static and the
 // runtime kernels (tools/kernel_lab.hip sweep, 256..1024 blocks); override
 // with HRS_BLOCKS_PER_CU for experiments.
-int blocks_per_cu() {
+// VALU-bound shapes (the rolled bit loop: 3-4 erasure repairs, wide
+// matrices) take 3 blocks per CU: the extra wave per SIMD hides more of the
+// math (RS(10,4) 4-erasure decode +13%, profiles/r01/pipe/).
+int blocks_per_cu(int dflt = 2) {
   static int v = [] {
     const char* e = getenv("HRS_BLOCKS_PER_CU");
     int x = e ? atoi(e) : 0;
-    return (x >= 1 && x <= 32) ? x : 2;
+    return (x >= 1 && x <= 32) ? x : 0;
   }();
-  return v;
+  return v ? v : dflt;
 }
 
-unsigned stream_grid(uint64_t ntasks) {
-  const uint64_t want = static_cast<uint64_t>(blocks_per_cu()) * device_cus();
+unsigned stream_grid(uint64_t ntasks, int per_cu = 2) {
+  const uint64_t want = static_cast<uint64_t>(blocks_per_cu(per_cu)) * device_cus();
   const uint64_t needed = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
   uint64_t g = needed < want ? needed : want;
   return static_cast<unsigned>(g == 0 ? 1 : g);
@@ -390,6 +471,19 @@ unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t ntasks)
   uint64_t g = needed < resident ? needed : resident;
   if (g == 0) g = 1;
   return static_cast<unsigned>(g);
+}
+
+// Software-pipelined runtime kernel for 1-2 outputs of <= 12 inputs (the 1-
+// and 2-erasure repairs: RS(10,4) 1-erasure decode +6-10%, 2 erasures
+// neutral); HRS_PIPE=0 selects the plain kernel for A/B runs. The same
+// pipelining of the static encode (-1%) and of the heterogeneous batch
+// kernel (-2%) measured slower and is not used (profiles/r01/pipe/ab2).
+bool use_pipe() {
+  static bool v = [] {
+    const char* e = getenv("HRS_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 template <int K, int P>
@@ -411,7 +505,10 @@ hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
 template <int NOUT, int NINB>
 hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_kernel<NOUT, NINB>;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
+  if constexpr (NOUT <= 2 && NINB <= 12)
+    if (use_pipe()) kern = bitsliced_pipe_kernel<NOUT, NINB>;
+  const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -429,7 +526,8 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
 template <int NOUT, int NINB>
 hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
   auto kern = batch_bitsliced_kernel<NOUT, NINB>;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
+  const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }
 
