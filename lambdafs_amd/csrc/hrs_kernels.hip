@@ -144,7 +144,8 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
         // output o), split in halves; the empty asm keeps the per-(o, b)
         // tests from being hoisted out of the task loop (they would spill).
         uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
-        asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
+        asm volatile("" : "+s"(cw[0]));
+        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
         // acc[o] ^= sum over set bits b of coef[o][r]: alpha^b * row
         if constexpr (BitLoop<NOUT, NINB>::kRolled) {
 #pragma unroll 1
@@ -208,7 +209,8 @@ __device__ __forceinline__ void apply_task(const RowArgs& a, uint64_t t, int nin
     if (r < nin) {
       bitslice(rows[r]);
       uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
-      asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
+      asm volatile("" : "+s"(cw[0]));
+        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
@@ -357,7 +359,8 @@ __global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const Ba
         bitslice(rows[r]);
         const uint64_t w = pl->cw[r];
         uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
-        asm volatile("" : "+s"(cw[0]), "+s"(cw[1]));
+        asm volatile("" : "+s"(cw[0]));
+        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
         if constexpr (BitLoop<NOUT, NINB>::kRolled) {
 #pragma unroll 1
           for (int b = 0; b < 8; ++b) {
