@@ -476,11 +476,15 @@ unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t ntasks)
   return static_cast<unsigned>(g);
 }
 
-// Software-pipelined runtime kernel for 1-2 outputs of <= 12 inputs (the 1-
-// and 2-erasure repairs: RS(10,4) 1-erasure decode +6-10%, 2 erasures
+// Software-pipelined runtime kernel for the unrolled shapes that fit (the 1-
+// to 3-erasure repairs: RS(10,4) 1-erasure decode +3-10%, 2-3 erasures
 // neutral); HRS_PIPE=0 selects the plain kernel for A/B runs. The same
 // pipelining of the static encode (-1%) and of the heterogeneous batch
 // kernel (-2%) measured slower and is not used (profiles/r01/pipe/ab2).
+// Unrolled shapes whose two row sets + accumulators fit 2 waves/SIMD.
+template <int NOUT, int NINB>
+constexpr bool kPipeFits = !BitLoop<NOUT, NINB>::kRolled && 16 * NINB + 8 * NOUT <= 232;
+
 bool use_pipe() {
   static bool v = [] {
     const char* e = getenv("HRS_PIPE");
@@ -508,7 +512,7 @@ hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
 template <int NOUT, int NINB>
 hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_kernel<NOUT, NINB>;
-  if constexpr (NOUT <= 2 && NINB <= 12)
+  if constexpr (kPipeFits<NOUT, NINB>)
     if (use_pipe()) kern = bitsliced_pipe_kernel<NOUT, NINB>;
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
