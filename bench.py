@@ -154,7 +154,8 @@ def stats(ms):
 # names as rocprofv3 reports them, keys of profiles/pmc_traffic.json.
 PIPE = os.environ.get("HRS_PIPE", "1") != "0"
 DEC_KERNEL = "bitsliced_pipe_kernel<1,12>" if PIPE else "bitsliced_kernel<1,12>"
-BATCH_KERNEL = "batch_bitsliced_kernel<1,12>"
+BATCH_KERNEL = ("batch_bitsliced_kernel<1,12,true>" if os.environ.get("HRS_BATCH_PATV", "1") != "0"
+                else "batch_bitsliced_kernel<1,12,false>")
 
 
 def enc_kernel_name(k, p):

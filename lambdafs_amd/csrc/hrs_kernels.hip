@@ -331,16 +331,32 @@ typedef const __attribute__((address_space(4))) int32_t* ConstIntPtr;
 
 // Same arithmetic as bitsliced_kernel; the wave reads its stripe's plan
 // (inputs, coefficients, output count) at the start of each task.
-template <int NOUT, int NINB>
+// PATV: lane l of the wave loads the pattern index of the wave's task
+// k + l (k = 0, 64, ...) in one vector load; each task then takes its index
+// with a readlane instead of a scalar load that waits on HBM before any of
+// the task's row loads can issue (the stripes of consecutive tasks differ).
+template <int NOUT, int NINB, bool PATV>
 __global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const BatchArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const ConstPlanPtr plans = (ConstPlanPtr)a.plans;
   const ConstIntPtr pat = (ConstIntPtr)a.pat;
-  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+  int patv = 0;
+  uint32_t k = 0;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves, ++k) {
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
-    const ConstPlanPtr pl = plans + pat[stripe];
+    int pidx;
+    if constexpr (PATV) {
+      if ((k & 63u) == 0) {
+        const uint64_t tl = t + static_cast<uint64_t>(lane) * nwaves;
+        patv = tl < a.ntasks ? a.pat[tl / a.nwin] : 0;
+      }
+      pidx = __builtin_amdgcn_readlane(patv, static_cast<int>(k & 63u));
+    } else {
+      pidx = pat[stripe];
+    }
+    const ConstPlanPtr pl = plans + pidx;
     const int nin = pl->nin;
     const int nout = pl->nout;
     const uint8_t* sb = a.base + stripe * a.stripe_stride + off;
@@ -530,9 +546,22 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// Batch kernel reads the pattern indices of its next 64 tasks with one
+// vector load (PATV) instead of a dependent scalar load per task;
+// HRS_BATCH_PATV=0 selects the per-task scalar read for A/B runs. (A
+// software-pipelined batch kernel like bitsliced_pipe_kernel measured 3-4%
+// slower, profiles/r01/pipe/batch_ab, and is not kept.)
+bool use_pat_prefetch() {
+  static bool v = [] {
+    const char* e = getenv("HRS_BATCH_PATV");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <int NOUT, int NINB>
 hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
-  auto kern = batch_bitsliced_kernel<NOUT, NINB>;
+  auto kern = use_pat_prefetch() ? batch_bitsliced_kernel<NOUT, NINB, true> : batch_bitsliced_kernel<NOUT, NINB, false>;
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();

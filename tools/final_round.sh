@@ -1,6 +1,6 @@
 # Round-end GPU pass: parity suite, smoke, per-code rates (pipelined and
 # plain runtime kernel), the rocprof round profile and the default bench line.
-mkdir -p gpurun_out/final3
+mkdir -p gpurun_out/final3 && rm -rf gpurun_out/prof
 timeout -k 10 300 python tools/sweep_apply.py > gpurun_out/final3/sweep.txt 2>&1 || exit $?
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/final3/gpu_tests.log 2>&1 || exit $?
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final3/smoke.log 2>&1 || exit $?

@@ -67,7 +67,8 @@ def main():
         with open(a.update) as fh:
             cur = json.load(fh)
         for k in ("encode_static_pipe_kernel<10,4>", "bitsliced_pipe_kernel<1,12>", "batch_pipe_kernel<1,12>",
-                  "encode_static_kernel<10,4>", "bitsliced_kernel<1,12>", "batch_bitsliced_kernel<1,12>"):
+                  "encode_static_kernel<10,4>", "bitsliced_kernel<1,12>", "batch_bitsliced_kernel<1,12>",
+                  "batch_bitsliced_kernel<1,12,true>", "batch_bitsliced_kernel<1,12,false>"):
             if k in table and "hbm_bytes_per_dispatch" in table[k]:
                 cur[k] = table[k]["hbm_bytes_per_dispatch"]
         cur["_note"] = (cur.get("_note", "").split("; source")[0] + "; source " + a.profile_dir + "/pmc_*/")
