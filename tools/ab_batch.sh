@@ -1,4 +1,4 @@
-# A/B of the pipelined batch kernel (HRS_PIPE_BATCH=0/1, both with the pattern prefetch), three alternating bench runs each.
+# A/B record: the pipelined batch kernel (HRS_PIPE_BATCH) measured neutral and was removed; this script produced profiles/r01/pipe/batch_ab_patv.
 OUT=gpurun_out/batchab3
 mkdir -p $OUT
 HRS_PIPE_BATCH=1 timeout -k 10 300 python -u -m pytest tests/test_batch_decode.py tests/test_gpu_exhaustive.py -x -q --timeout 120 --timeout-method thread > $OUT/batch_tests_pipe.log 2>&1 || exit $?
