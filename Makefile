@@ -11,9 +11,10 @@ ORACLE   := oracle/liboracle.so
 HDRS     := include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
             lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
 
-HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model
+JNI      := lambdafs_amd/libhrs_jni.so
+HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness
 
-all: $(LIB) $(ORACLE) $(HARNESS)
+all: $(LIB) $(ORACLE) $(JNI) $(HARNESS)
 
 build/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS)
 	@mkdir -p build
@@ -39,13 +40,24 @@ $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
 
 # Test-only native harness (tests/cpp): the codec driven like Encoder/Decoder.
 tests/cpp/codec_harness: tests/cpp/codec_harness.cpp include/hrs.hpp include/hrs.h $(LIB) $(ORACLE)
-	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs -Loracle -loracle -lz \
+	g++ -O2 -std=c++17 -Wall -pthread -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs -Loracle -loracle -lz \
+	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# The JNI shim, compiled against the hand-declared JNI ABI subset
+# (lambdafs_amd/jni/jni_min.h; -DHRS_SYSTEM_JNI + JDK include dirs for <jni.h>).
+$(JNI): lambdafs_amd/jni/hrs_jni.c lambdafs_amd/jni/jni_min.h include/hrs.h $(LIB)
+	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -Werror -Iinclude -o $@ $< -Llambdafs_amd -lhrs \
+	    -Wl,-rpath,'$$ORIGIN'
+
+# Fake-JVM harness driving every HrsNative entry point (tests/test_jni.py).
+tests/cpp/jni_harness: tests/cpp/jni_harness.c lambdafs_amd/jni/jni_min.h $(JNI) $(ORACLE)
+	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs_jni -lhrs -Loracle -loracle -lz \
 	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
 	g++ -O2 -std=c++17 -Wall -o $@ $< -lz
 
 clean:
-	rm -rf build $(LIB) $(ORACLE) $(HARNESS)
+	rm -rf build $(LIB) $(ORACLE) $(JNI) $(HARNESS)
 
 .PHONY: all clean

@@ -46,6 +46,8 @@ struct hrs_codec {
   std::map<uint64_t, uint32_t*> crc_fold_tables;
   uint32_t* crc_raw = nullptr;
   size_t crc_raw_bytes = 0;
+  hipEvent_t crc_raw_done = nullptr;  // recorded after the latest use (crc_scratch)
+  bool crc_raw_used = false;
   std::map<uint64_t, hrs::crc::Mat> crc_zmats;  // host-side Z_len, chaining chunk CRCs
   // hrs_decode_batch_dev: two slots (plans + per-stripe pattern index), each
   // a device buffer and its pinned staging; a slot is reused once the event
@@ -490,6 +492,11 @@ hrs_status decode5_matrix(hrs_codec* c, const int* erased, int ne, const int* nt
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// The compile-time encode kernels hold the hops RS generator (rs) or the
+// ISA-L Cauchy rows (nrs) of a (k, p) shape; only those families' G may take
+// them. SRC's G (XOR groups over RS(k, r)) and XOR's all-ones row may not.
+bool static_encode_family(const hrs_codec* c) { return c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS; }
+
 // out_o = XOR_i m[o][i] * in_i for every stripe. `static_kp` allows the
 // compile-time encode kernels when m is this codec's G and inputs are the k
 // data rows in order.
@@ -511,7 +518,7 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
       live.push_back(i);
     }
   }
-  if (static_cast<int>(live.size()) != nin) static_kp = false;
+  if (static_cast<int>(live.size()) != nin || !static_encode_family(c) || m != c->g.data()) static_kp = false;
   bool vec_ok = (in_stride % 16 == 0) && (out_stride % 16 == 0);
   for (int i : live) vec_ok &= aligned16(in_rows[i]);
   for (int o = 0; o < nout; ++o) vec_ok &= aligned16(out_rows[o]);
@@ -700,8 +707,8 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
   return it->second;
 }
 
-hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
-                      uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc = HostCrc()) {
+hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                           uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc) {
   const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
   if (ncrc > 0) {  // the running values; an empty call leaves them as they are
     for (int r = 0; r < ncrc; ++r) crc.out[r] = crc.in ? crc.in[r] : 0u;
@@ -799,6 +806,19 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   return HRS_OK;
 }
 
+// A call that fails part-way may leave a slot's H2D / kernel / D2H in
+// flight; the next call would then memcpy into staging the DMA engine is
+// still reading or writing. So a failed call drains both slot streams before
+// it returns (a successful one has already waited for every slot it used).
+hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                      uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc = HostCrc()) {
+  const hrs_status st = host_apply_impl(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc);
+  if (st != HRS_OK)
+    for (auto& h : c->host)
+      if (h.stream) (void)hipStreamSynchronize(h.stream);
+  return st;
+}
+
 void init_encode_matrix(hrs_codec* c) {
   c->g.resize(static_cast<size_t>(c->p) * c->k);
   if (c->kind == HRS_CODE_XOR) {
@@ -871,20 +891,45 @@ hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, const uint32_t** out) {
   return HRS_OK;
 }
 
-// Raw-CRC scratch of at least `bytes` (the fold reads it after the window pass).
+// Raw-CRC scratch of at least `bytes` (the fold reads it after the window
+// pass), shared by every device CRC call on this handle whatever its stream.
+// Uses are chained: a call on stream s first waits (on the GPU) for the event
+// recorded after the previous use, and records it again when its own
+// launches are queued (crc_scratch_release). So the last event covers every
+// earlier use, and growing the buffer waits for that event before hipFree.
 hrs_status crc_scratch(hrs_codec* c, size_t bytes, hipStream_t s) {
   bytes = std::max<size_t>(4, bytes);
-  if (c->crc_raw_bytes >= bytes) return HRS_OK;
-  if (c->crc_raw) {
-    (void)hipStreamSynchronize(s);
-    (void)hipFree(c->crc_raw);
-    c->crc_raw = nullptr;
-    c->crc_raw_bytes = 0;
+  if (!c->crc_raw_done) {
+    hipError_t e = hipEventCreateWithFlags(&c->crc_raw_done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
   }
-  hipError_t e = hipMalloc(&c->crc_raw, bytes);
-  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
-  c->crc_raw_bytes = bytes;
+  if (c->crc_raw_bytes < bytes) {
+    if (c->crc_raw) {
+      if (c->crc_raw_used) {
+        hipError_t e = hipEventSynchronize(c->crc_raw_done);
+        if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
+      }
+      (void)hipFree(c->crc_raw);
+      c->crc_raw = nullptr;
+      c->crc_raw_bytes = 0;
+      c->crc_raw_used = false;
+    }
+    hipError_t e = hipMalloc(&c->crc_raw, bytes);
+    if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    c->crc_raw_bytes = bytes;
+  }
+  if (c->crc_raw_used) {
+    hipError_t e = hipStreamWaitEvent(s, c->crc_raw_done, 0);
+    if (e != hipSuccess) return hip_fail(c, e, "hipStreamWaitEvent");
+  }
   return HRS_OK;
+}
+
+hrs_status crc_scratch_release(hrs_codec* c, hipStream_t s, hrs_status st) {
+  hipError_t e = hipEventRecord(c->crc_raw_done, s);
+  if (e != hipSuccess) return st != HRS_OK ? st : hip_fail(c, e, "hipEventRecord");
+  c->crc_raw_used = true;
+  return st;
 }
 
 // Folds the raw window CRCs of nsr (stripe, row) pairs into CRC32 values.
@@ -989,7 +1034,7 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
   }
   // two passes: encode, then the CRC of the k sources and p parities
   hrs_status st = run_apply(c, c->g.data(), p, k, in_rows, in_stride, out_rows, out_stride, len, nstripes, s,
-                            c->kind != HRS_CODE_XOR);
+                            static_encode_family(c));
   if (st != HRS_OK) return st;
   std::vector<const uint8_t*> rows(n);
   std::vector<size_t> strides(n);
@@ -1021,7 +1066,8 @@ hrs_status hrs_crc32_dev(hrs_codec* c, const uint8_t* const* rows, int nrows, si
   hipStream_t s = static_cast<hipStream_t>(stream);
   hrs_status st = crc_scratch(c, crc_raw_bytes_for(len, nstripes, nrows), s);
   if (st != HRS_OK) return st;
-  return run_crc(c, rows, strides.data(), nrows, len, nstripes, crc_in, crc_out, s, c->crc_raw);
+  return crc_scratch_release(c, s, run_crc(c, rows, strides.data(), nrows, len, nstripes, crc_in, crc_out, s,
+                                           c->crc_raw));
 }
 
 hrs_status hrs_encode_crc_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
@@ -1039,7 +1085,8 @@ hrs_status hrs_encode_crc_dev(hrs_codec* c, const uint8_t* const* in_rows, size_
   hipStream_t s = static_cast<hipStream_t>(stream);
   hrs_status st = crc_scratch(c, crc_raw_bytes_for(len, nstripes, c->n), s);
   if (st != HRS_OK) return st;
-  return encode_crc_impl(c, in_rows, in_stride, out_rows, out_stride, len, nstripes, crc_in, crc_out, s, c->crc_raw);
+  return crc_scratch_release(
+      c, s, encode_crc_impl(c, in_rows, in_stride, out_rows, out_stride, len, nstripes, crc_in, crc_out, s, c->crc_raw));
 }
 
 const char* hrs_version(void) { return "hrs 0.1.0 (gfx950)"; }
@@ -1150,6 +1197,10 @@ void hrs_destroy(hrs_codec* c) {
   }
   if (c->crc_tables_a) (void)hipFree(c->crc_tables_a);
   for (auto& kv : c->crc_fold_tables) (void)hipFree(kv.second);
+  if (c->crc_raw_done) {
+    (void)hipEventSynchronize(c->crc_raw_done);
+    (void)hipEventDestroy(c->crc_raw_done);
+  }
   if (c->crc_raw) (void)hipFree(c->crc_raw);
   for (auto& h : c->host) {
     if (h.stream) {
@@ -1258,7 +1309,7 @@ hrs_status hrs_decode_matrix(const hrs_codec* cc, const int* erased, int ne, con
 hrs_status hrs_encode(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
   if (!c) return HRS_EINVAL;
   if (!inputs || !outputs) return fail(c, HRS_EINVAL, "inputs/outputs is NULL");
-  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind != HRS_CODE_XOR);
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, static_encode_family(c));
 }
 
 hrs_status hrs_encode_crc(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len,
@@ -1269,7 +1320,7 @@ hrs_status hrs_encode_crc(hrs_codec* c, const uint8_t* const* inputs, uint8_t* c
   crc.mode = kCrcEncode;
   crc.in = crc_in;
   crc.out = crc_out;
-  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, c->kind != HRS_CODE_XOR, crc);
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, static_encode_family(c), crc);
 }
 
 hrs_status hrs_decode_crc(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
@@ -1339,7 +1390,7 @@ hrs_status hrs_encode_dev(hrs_codec* c, const uint8_t* const* in_rows, size_t in
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   return run_apply(c, c->g.data(), c->p, c->k, in_rows, in_stride, out_rows, out_stride, len, nstripes,
-                   static_cast<hipStream_t>(stream), c->kind != HRS_CODE_XOR);
+                   static_cast<hipStream_t>(stream), static_encode_family(c));
 }
 
 hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_stride, uint8_t* const* out_rows,
@@ -1427,6 +1478,9 @@ hrs_status hrs_decode_batch_dev(hrs_codec* c, const uint8_t* stripes, size_t row
     mats.push_back(std::move(m));
     pat[s] = id;
   }
+  // one launch covers every pattern at (max_nout, max_nin): a wide pattern
+  // (6-8 outputs) and a many-input one (> 8 inputs) cannot share it
+  if (max_nout > 5 && max_nin > hrs::kMaxInRuntimeWide) fused = false;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   hipStream_t hs = static_cast<hipStream_t>(stream);

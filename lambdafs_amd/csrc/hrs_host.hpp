@@ -3,7 +3,15 @@
 // heap array), are copied by a few threads into pinned staging, and DMA'd from
 // there, chunk by chunk, while the GPU works on the previous chunk
 // (hrs_api.cpp: host_apply).
+//
+// Several codec handles may call concurrently (one codec per mapper / repair
+// thread: Encoder.java:80, Decoder.java:90, MapReduceBlockRepairManager.java:426),
+// so run() never serializes callers: each call posts its pieces as a batch,
+// copies its own pieces on the calling thread, and the shared workers take
+// pieces from every open batch in turn. A call returns once all its pieces
+// are copied and no worker still holds its batch.
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstddef>
@@ -22,8 +30,6 @@ struct CopyJob {
   size_t bytes;
 };
 
-// A fixed set of worker threads; run() splits the jobs into <= 256 KiB
-// pieces, the caller joins in, and returns when every byte is copied.
 class CopyPool {
  public:
   static CopyPool& instance() {
@@ -38,30 +44,27 @@ class CopyPool {
       for (const CopyJob& j : jobs) std::memcpy(j.dst, j.src, j.bytes);
       return;
     }
-    std::lock_guard<std::mutex> one_at_a_time(run_mu_);
-    pieces_.clear();
+    Batch b;
     for (const CopyJob& j : jobs)
       for (size_t off = 0; off < j.bytes; off += kPiece) {
-        const size_t b = j.bytes - off < kPiece ? j.bytes - off : kPiece;
-        pieces_.push_back({static_cast<uint8_t*>(j.dst) + off, static_cast<const uint8_t*>(j.src) + off, b});
+        const size_t n = std::min(kPiece, j.bytes - off);
+        b.pieces.push_back({static_cast<uint8_t*>(j.dst) + off, static_cast<const uint8_t*>(j.src) + off, n});
       }
-    next_.store(0);
     {
       std::lock_guard<std::mutex> lk(mu_);
-      busy_ = nthreads_;
-      ++generation_;
+      open_.push_back(&b);
     }
     cv_.notify_all();
-    drain();
+    drain(b);
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return busy_ == 0; });
+    close(&b);  // no new worker may join
+    done_cv_.wait(lk, [&] { return b.users == 0 && b.done.load() == b.pieces.size(); });
   }
 
   ~CopyPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
-      ++generation_;
     }
     cv_.notify_all();
     for (std::thread& t : threads_) t.join();
@@ -70,46 +73,70 @@ class CopyPool {
  private:
   static constexpr size_t kPiece = 256u << 10;
 
+  struct Batch {
+    std::vector<CopyJob> pieces;
+    std::atomic<size_t> next{0};
+    std::atomic<size_t> done{0};
+    int users = 0;  // workers inside drain(); guarded by mu_
+  };
+
   CopyPool() {
     const char* e = getenv("HRS_HOST_THREADS");
-    int n = e ? atoi(e) : 2;  // measured best on the MI355X hosts (tools/host_sweep.sh)
+    int n = e ? atoi(e) : 2;  // measured best for one caller on the MI355X hosts (tools/host_sweep.sh)
     if (n < 0) n = 0;
     if (n > 32) n = 32;
     nthreads_ = n;
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker(); });
   }
 
-  void drain() {
+  // Copies pieces of b until none is left unclaimed.
+  static void drain(Batch& b) {
     for (;;) {
-      const size_t i = next_.fetch_add(1);
-      if (i >= pieces_.size()) return;
-      std::memcpy(pieces_[i].dst, pieces_[i].src, pieces_[i].bytes);
+      const size_t i = b.next.fetch_add(1);
+      if (i >= b.pieces.size()) return;
+      std::memcpy(b.pieces[i].dst, b.pieces[i].src, b.pieces[i].bytes);
+      b.done.fetch_add(1);
     }
   }
 
+  void close(Batch* b) {  // mu_ held
+    auto it = std::find(open_.begin(), open_.end(), b);
+    if (it != open_.end()) open_.erase(it);
+  }
+
   void worker() {
-    uint64_t seen = 0;
+    size_t turn = 0;
     for (;;) {
+      Batch* b = nullptr;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return generation_ != seen; });
-        seen = generation_;
+        cv_.wait(lk, [&] { return stop_ || !open_.empty(); });
         if (stop_) return;
+        b = open_[turn++ % open_.size()];  // interleave concurrent callers
+        if (b->next.load() >= b->pieces.size()) {
+          close(b);  // fully claimed: its caller finishes it
+          continue;
+        }
+        ++b->users;
       }
-      drain();
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--busy_ == 0) done_cv_.notify_all();
+      const size_t i = b->next.fetch_add(1);
+      if (i < b->pieces.size()) {
+        std::memcpy(b->pieces[i].dst, b->pieces[i].src, b->pieces[i].bytes);
+        b->done.fetch_add(1);
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --b->users;
+      }
+      done_cv_.notify_all();
     }
   }
 
   int nthreads_ = 0;
   std::vector<std::thread> threads_;
-  std::vector<CopyJob> pieces_;
-  std::atomic<size_t> next_{0};
-  std::mutex run_mu_, mu_;
+  std::vector<Batch*> open_;
+  std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  uint64_t generation_ = 0;
-  int busy_ = 0;
   bool stop_ = false;
 };
 

@@ -23,6 +23,8 @@
 // The bit-slice transform is an involution, applied again to the outputs.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cstdlib>
 
 #include "hrs_device.hpp"
@@ -437,22 +439,19 @@ __global__ void __launch_bounds__(kBlockThreads) batch_bytewise_kernel(const Bat
 
 // ------------------------------------------------------------ launching
 
-struct DeviceInfo {
-  int cus = 0;
-};
-
+// CU count per device, cached; handles on several host threads may race to
+// fill it (same value), hence the relaxed atomics.
 int device_cus() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
-  static DeviceInfo infos[64];
+  static std::atomic<int> cus_of[64];
   if (dev < 0 || dev >= 64) return 256;
-  if (infos[dev].cus == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    infos[dev].cus = cus;
+  int cus = cus_of[dev].load(std::memory_order_relaxed);
+  if (cus == 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cus_of[dev].store(cus, std::memory_order_relaxed);
   }
-  return infos[dev].cus;
+  return cus;
 }
 
 // Streaming kernels: a fixed number of resident blocks per CU, grid-striding

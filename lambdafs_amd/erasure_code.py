@@ -189,6 +189,19 @@ class _HipErasureCode(ErasureCode):
     def _check(self, st):
         check(st, self._h)
 
+    def _placement(self, *row_sets):
+        """Where a bulk call runs: None (host rows) or the device ordinal.
+        Every row set must agree (a kernel storing to host addresses faults
+        the GPU; a host memcpy into device pointers segfaults), and device
+        rows must sit on the codec's device when it names one."""
+        devs = {r.device for r in row_sets if r.len > 0 or r.device is not None}
+        if len(devs) > 1:
+            raise ValueError("bulk rows must all be host buffers or all on one device")
+        dev = devs.pop() if devs else None
+        if dev is not None and self._device is not None and int(self._device) != dev:
+            raise ValueError(f"rows are on cuda:{dev} but the codec is on cuda:{int(self._device)}")
+        return dev
+
     # -- geometry
     def stripeSize(self):
         return self._k
@@ -240,9 +253,7 @@ class _HipErasureCode(ErasureCode):
         if ins.len != outs.len:
             raise ValueError("input and output rows differ in length")
         L = _lib.lib()
-        if ins.device is not None or outs.device is not None:
-            if ins.device != outs.device:
-                raise ValueError("encodeBulk rows must all be on one device")
+        if self._placement(ins, outs) is not None:
             stream = _lib.torch.cuda.current_stream(ins.device).cuda_stream
             self._check(L.hrs_encode_dev(self._handle(), ins.ptrs, 0, outs.ptrs, 0, ins.len, 1, stream))
             return
@@ -268,7 +279,7 @@ class _HipErasureCode(ErasureCode):
                 return
             reads = _Rows(readBufs, writable=False)
             writes = _Rows(writeBufs, writable=True)
-            if reads.device is not None:
+            if self._placement(reads, writes) is not None:
                 if self.CODE_KIND == _lib.HRS_CODE_XOR:
                     m = self.decodeMatrix(erasedLocations, [])
                 else:
@@ -284,9 +295,10 @@ class _HipErasureCode(ErasureCode):
         reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
                       writable=False, allow_none=True)
         writes = _Rows(writeBufs, writable=True)
+        where = self._placement(reads, writes)
         if not erasedLocations and self.CODE_KIND == _lib.HRS_CODE_RS:
             return
-        if reads.device is not None:
+        if where is not None:
             stream = _lib.torch.cuda.current_stream(reads.device).cuda_stream
             self._check(L.hrs_decode_dev(
                 self._handle(), reads.ptrs, 0, writes.ptrs, 0, int_array(erasedLocations), len(erasedLocations),
@@ -319,7 +331,7 @@ class _HipErasureCode(ErasureCode):
         outs = _Rows(outputs, writable=True)
         if ins.len != outs.len:
             raise ValueError("input and output rows differ in length")
-        if ins.device is not None or outs.device is not None:
+        if self._placement(ins, outs) is not None:
             raise ValueError("encodeBulkCrc takes host rows (device rows: device.encode_crc_stripes)")
         crc_in, crc_out = self._crc_arrays(crcs, self._k + self._p)
         self._check(_lib.lib().hrs_encode_crc(self._handle(), ins.ptrs, outs.ptrs, ins.len,
@@ -343,7 +355,7 @@ class _HipErasureCode(ErasureCode):
         reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
                       writable=False, allow_none=True)
         writes = _Rows(writeBufs, writable=True)
-        if reads.device is not None:
+        if self._placement(reads, writes) is not None:
             raise ValueError("decodeBulkCrc takes host rows")
         crc_in, crc_out = self._crc_arrays(crcs, len(erasedLocations))
         if not erasedLocations:

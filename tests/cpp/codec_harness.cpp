@@ -21,11 +21,25 @@
 // oracle's orc_nrs_decode_bulk, and the repaired CRC against the block the Java
 // actually returns in writeBufs[i] (the i-th not-to-read location in Apache
 // order; "quirk" says whether that differs from erasedLocations[i]).
+// --grow=R : Decoder restart (Decoder.java:373-387, readFromInputs :403-436):
+// one block (erased[0]) is repaired; at round R a read of one of the
+// locations to read fails (BlockMissingException), that location joins
+// erasedLocations, the three arrays are rebuilt and the round is redone from
+// the same offset. The repaired block and its CRC32 (chained across the
+// pattern change) must match the stored ones; the decode-matrix cache must
+// hand out the new pattern's matrix.
+// --threads=N [--rounds=M] : N threads, one codec handle each (Encoder.java:80,
+// Decoder.java:90: one ErasureCode per task), interleaving encodeBulk and
+// decodeBulk of bufSize cells of RS(k,p); a checked pass (every round vs the
+// oracle's parity / the original cells) then a timed pass; prints the
+// aggregate user-data GiB/s (k * bufSize per call).
 // Prints one JSON line; exit status 0 iff everything matched.
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <memory>
 #include <cstdio>
 #include <cstdlib>
@@ -83,9 +97,184 @@ int host_only_checks(int k, int p) {
 
 }  // namespace
 
+
+bool contains(const std::vector<int>& v, int x) {
+  for (int y : v)
+    if (y == x) return true;
+  return false;
+}
+
+// Decoder.java:303-338: ascending erased / toRead / notToRead arrays.
+void decoder_arrays(int n, const std::vector<int>& erased, const std::vector<int>& to_read, std::vector<int>& ea,
+                    std::vector<int>& ta, std::vector<int>& na) {
+  ea.clear();
+  ta.clear();
+  na.clear();
+  for (int loc = 0; loc < n; ++loc)
+    if (contains(erased, loc)) ea.push_back(loc);
+  for (int loc = 0; loc < n; ++loc)
+    if (contains(to_read, loc)) ta.push_back(loc);
+  for (int loc = 0; loc < n; ++loc)
+    if (!contains(to_read, loc) || contains(erased, loc)) na.push_back(loc);
+}
+
+// --grow: one block repaired, a second location lost at round `grow_round`.
+int grow_mode(int k, int p, size_t block, size_t buf, int grow_round, uint64_t seed) {
+  const int n = k + p;
+  hrs::HipReedSolomonCode code(k, p, 0);
+  std::vector<std::vector<uint8_t>> stripe(n, std::vector<uint8_t>(block));
+  for (int i = 0; i < k; ++i) fill(stripe[p + i], seed * 1000 + i);
+  {  // parity by the oracle (it zeroes its inputs: copies)
+    std::vector<std::vector<uint8_t>> cp(stripe.begin() + p, stripe.end());
+    std::vector<uint8_t*> ip(k), op(p);
+    for (int i = 0; i < k; ++i) ip[i] = cp[i].data();
+    for (int r = 0; r < p; ++r) op[r] = stripe[r].data();
+    orc_rs_encode_bulk(k, p, ip.data(), op.data(), block);
+  }
+  std::vector<uint32_t> stored(n, 0);
+  for (int l = 0; l < n; ++l) stored[l] = crc(0, stripe[l].data(), block);
+  uint64_t s = seed;
+  const int to_fix = p + static_cast<int>(splitmix(s) % k);  // a data block
+  std::vector<int> erased = {to_fix};
+  std::vector<int> to_read = code.locationsToReadForDecode(erased);
+  // the location whose read fails mid-block: one the decoder is reading
+  const int lost_later = to_read[static_cast<size_t>(splitmix(s) % to_read.size())];
+  std::vector<int> ea, ta, na;
+  decoder_arrays(n, erased, to_read, ea, ta, na);
+  std::vector<uint8_t> repaired(block);
+  uint32_t fix_crc = 0;           // java.util.zip.CRC32 of the repaired block (host zlib)
+  uint32_t gpu_fix_crc = 0;       // the engine's running value (decodeBulkCrc)
+  size_t mismatches = 0, restarts = 0, rounds = 0;
+  int patterns = 1;
+  size_t written = 0;
+  while (written < block) {
+    const size_t len = std::min(buf, block - written);
+    if (restarts == 0 && rounds == static_cast<size_t>(grow_round)) {
+      // readFromInputs: BlockMissingException in stream lost_later ->
+      // erasedLocations.add, rebuild inputs from the same offset
+      erased.push_back(lost_later);
+      to_read = code.locationsToReadForDecode(erased);
+      decoder_arrays(n, erased, to_read, ea, ta, na);
+      ++restarts;
+      ++patterns;
+    }
+    std::vector<std::vector<uint8_t>> read(n, std::vector<uint8_t>(len, 0));
+    std::vector<uint8_t*> rp(n);
+    for (int l = 0; l < n; ++l) {
+      if (contains(ta, l) && !contains(ea, l)) std::memcpy(read[l].data(), stripe[l].data() + written, len);
+      rp[l] = read[l].data();
+    }
+    const int ne = static_cast<int>(ea.size());
+    std::vector<std::vector<uint8_t>> wb(ne, std::vector<uint8_t>(buf));
+    std::vector<uint8_t*> wp(ne);
+    for (int i = 0; i < ne; ++i) wp[i] = wb[i].data();
+    std::vector<uint32_t> crcs(ne, 0);
+    int fix_idx = -1;
+    for (int i = 0; i < ne; ++i)
+      if (ea[i] == to_fix) fix_idx = i;
+    crcs[fix_idx] = gpu_fix_crc;
+    code.decodeBulkCrc(rp, wp, len, ea, ta, na, crcs);
+    gpu_fix_crc = crcs[fix_idx];
+    for (int i = 0; i < ne; ++i)  // every erased cell of the round is right
+      mismatches += std::memcmp(wb[i].data(), stripe[ea[i]].data() + written, len) != 0;
+    std::memcpy(repaired.data() + written, wb[fix_idx].data(), len);  // out.write(writeBufs[i]) (:360-372)
+    fix_crc = crc(fix_crc, wb[fix_idx].data(), len);
+    written += len;
+    ++rounds;
+  }
+  const bool block_ok = std::memcmp(repaired.data(), stripe[to_fix].data(), block) == 0;
+  const bool ok = block_ok && mismatches == 0 && fix_crc == stored[to_fix] && gpu_fix_crc == fix_crc && restarts == 1;
+  printf("{\"mode\": \"grow\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"to_fix\": %d, \"lost_later\": %d, "
+         "\"grow_round\": %d, \"rounds\": %zu, \"restarts\": %zu, \"patterns\": %d, \"round_mismatches\": %zu, "
+         "\"block_ok\": %s, \"crc_ok\": %s, \"gpu_crc_ok\": %s, \"ok\": %s}\n",
+         k, p, block, buf, to_fix, lost_later, grow_round, rounds, restarts, patterns, mismatches,
+         block_ok ? "true" : "false", fix_crc == stored[to_fix] ? "true" : "false",
+         gpu_fix_crc == fix_crc ? "true" : "false", ok ? "true" : "false");
+  return ok ? 0 : 1;
+}
+
+// --threads: concurrent handles.
+int threads_mode(int k, int p, size_t buf, int nthreads, int rounds, uint64_t seed) {
+  const int n = k + p;
+  const int nstripes = 4;
+  // stripes + oracle parity, shared read-only by every thread
+  std::vector<std::vector<std::vector<uint8_t>>> st(nstripes, std::vector<std::vector<uint8_t>>(n, std::vector<uint8_t>(buf)));
+  for (int s = 0; s < nstripes; ++s) {
+    for (int i = 0; i < k; ++i) fill(st[s][p + i], seed * 1000 + 100 * s + i);
+    std::vector<std::vector<uint8_t>> cp(st[s].begin() + p, st[s].end());
+    std::vector<uint8_t*> ip(k), op(p);
+    for (int i = 0; i < k; ++i) ip[i] = cp[i].data();
+    for (int r = 0; r < p; ++r) op[r] = st[s][r].data();
+    orc_rs_encode_bulk(k, p, ip.data(), op.data(), buf);
+  }
+  std::atomic<size_t> bad{0}, errors{0};
+  std::atomic<int> ready{0};
+  std::atomic<bool> go{false};
+  double timed_s = 0;
+  auto body = [&](int t, bool check) {
+    try {
+      hrs::HipReedSolomonCode code(k, p, 0);
+      std::vector<std::vector<uint8_t>> par(p, std::vector<uint8_t>(buf)), wb(p, std::vector<uint8_t>(buf));
+      std::vector<uint8_t*> pp(p), wp;
+      for (int r = 0; r < p; ++r) pp[r] = par[r].data();
+      // warm-up (not timed): the handle's staging slots and matrices
+      for (int i = -2; i < rounds; ++i) {
+        if (i == 0) {
+          ready.fetch_add(1);
+          while (!go.load()) std::this_thread::yield();
+        }
+        const int s = (t + i + nstripes) % nstripes;
+        std::vector<uint8_t*> in(k);
+        for (int c = 0; c < k; ++c) in[c] = st[s][p + c].data();
+        code.encodeBulk(in, pp, buf);
+        if (check)
+          for (int r = 0; r < p; ++r) bad += std::memcmp(par[r].data(), st[s][r].data(), buf) != 0;
+        // lose 1..p locations (varies per round and thread: the cache sees many patterns)
+        std::vector<int> erased;
+        uint64_t z = seed + 7919u * t + static_cast<uint64_t>(i + 2);
+        const int ne = 1 + static_cast<int>(splitmix(z) % p);
+        while (static_cast<int>(erased.size()) < ne) {
+          const int loc = static_cast<int>(splitmix(z) % n);
+          if (!contains(erased, loc)) erased.push_back(loc);
+        }
+        std::vector<int> ea, ta, na;
+        decoder_arrays(n, erased, code.locationsToReadForDecode(erased), ea, ta, na);
+        std::vector<uint8_t*> rp(n, nullptr);
+        for (int l : ta) rp[l] = st[s][l].data();  // not-to-read rows are never read: NULL
+        wp.assign(ea.size(), nullptr);
+        for (size_t j = 0; j < ea.size(); ++j) wp[j] = wb[j].data();
+        code.decodeBulk(rp, wp, buf, ea, ta, na);
+        if (check)
+          for (size_t j = 0; j < ea.size(); ++j) bad += std::memcmp(wb[j].data(), st[s][ea[j]].data(), buf) != 0;
+      }
+    } catch (const std::exception& e) {
+      fprintf(stderr, "thread %d: %s\n", t, e.what());
+      errors.fetch_add(1);
+    }
+  };
+  for (int pass = 0; pass < 2; ++pass) {  // 0: every round checked; 1: timed
+    ready = 0;
+    go = false;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) th.emplace_back(body, t, pass == 0);
+    while (ready.load() < nthreads && errors.load() == 0) std::this_thread::yield();
+    const auto t0 = std::chrono::steady_clock::now();
+    go = true;
+    for (auto& x : th) x.join();
+    if (pass == 1) timed_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  const double user = 2.0 * k * static_cast<double>(buf) * rounds * nthreads;  // encode + decode, k cells each
+  const bool ok = bad == 0 && errors == 0;
+  printf("{\"mode\": \"threads\", \"k\": %d, \"p\": %d, \"buf\": %zu, \"threads\": %d, \"rounds\": %d, "
+         "\"mismatches\": %zu, \"errors\": %zu, \"seconds\": %.4f, \"aggregate_GiBps\": %.3f, \"ok\": %s}\n",
+         k, p, buf, nthreads, rounds, bad.load(), errors.load(), timed_s, user / (1u << 30) / timed_s,
+         ok ? "true" : "false");
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   bool host_only = false, use_xor = false, use_nrs = false, use_src = false;
-  int src_s = 0;
+  int src_s = 0, grow = -1, threads = 0, rounds = 16;
   std::vector<std::string> pos;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -95,6 +284,12 @@ int main(int argc, char** argv) {
       use_xor = true;
     else if (a == "--nrs")
       use_nrs = true;
+    else if (a.rfind("--grow=", 0) == 0)
+      grow = atoi(a.c_str() + 7);
+    else if (a.rfind("--threads=", 0) == 0)
+      threads = atoi(a.c_str() + 10);
+    else if (a.rfind("--rounds=", 0) == 0)
+      rounds = atoi(a.c_str() + 9);
     else if (a.rfind("--src=", 0) == 0) {
       use_src = true;
       src_s = atoi(a.c_str() + 6);
@@ -109,6 +304,13 @@ int main(int argc, char** argv) {
   const int nerased = pos.size() > 4 ? atoi(pos[4].c_str()) : 1;
   const uint64_t seed = pos.size() > 5 ? strtoull(pos[5].c_str(), nullptr, 10) : 7;
   if (host_only) return host_only_checks(k, p);
+  try {
+    if (grow >= 0) return grow_mode(k, p, block, buf, grow, seed);
+    if (threads > 0) return threads_mode(k, p, buf, threads, rounds, seed);
+  } catch (const std::exception& e) {
+    printf("{\"error\": \"%s\", \"ok\": false}\n", e.what());
+    return 2;
+  }
   const int n = k + p;
 
   try {
@@ -185,11 +387,6 @@ int main(int argc, char** argv) {
         if (!use_src) throw;
       }
     }
-    auto contains = [](const std::vector<int>& v, int x) {
-      for (int y : v)
-        if (y == x) return true;
-      return false;
-    };
     std::vector<int> erased_arr, to_read_arr, ntr_arr;  // Decoder.java:303-338
     for (int loc = 0; loc < n; ++loc)
       if (contains(erased_list, loc)) erased_arr.push_back(loc);

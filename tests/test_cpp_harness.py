@@ -63,3 +63,33 @@ def test_harness_src(cuda, nerased, seed):
     # equal to the oracle's transcription, repaired CRCs equal to the stored ones
     rc, res = run("--src=2", 10, 6, 3 << 20, 1 << 20, nerased, seed)
     assert rc == 0 and res["ok"], res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    (10, 4, 4 << 20, 1 << 20, 2, 21),            # lost at round 2 of 4
+    (12, 4, 2 << 20, 256 << 10, 3, 22),          # RS(12,4), 256 KiB cells, round 3 of 8
+    (6, 3, (3 << 20) + 4097, 1 << 20, 3, 23),    # the partial last round
+    (10, 4, 4 << 20, 1 << 20, 0, 24),            # lost in the very first round
+])
+def test_harness_decoder_restart_mid_block(cuda, args):
+    """Decoder.java:373-387: a read error mid-block adds an erased location,
+    the arrays are rebuilt and the round is redone; the repaired block and its
+    chained CRC32 must equal the stored ones (the decode-matrix cache is keyed
+    on the new pattern)."""
+    k, p, block, buf, grow, seed = args
+    rc, res = run(f"--grow={grow}", k, p, block, buf, 1, seed)
+    assert rc == 0 and res["ok"], res
+    assert res["restarts"] == 1 and res["patterns"] == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [2, 4])
+def test_harness_concurrent_handles(cuda, threads):
+    """One codec per thread (Encoder.java:80, Decoder.java:90,
+    MapReduceBlockRepairManager.java:426): threads interleave encodeBulk and
+    decodeBulk (1-4 lost locations, changing every round) of RS(10,4) 1 MiB
+    cells on their own handles; every round bit-exact vs the oracle's parity
+    and the original cells."""
+    rc, res = run(f"--threads={threads}", "--rounds=12", 10, 4, 1 << 20, 1 << 20, 1, 31)
+    assert rc == 0 and res["ok"], res

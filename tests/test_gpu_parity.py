@@ -197,6 +197,34 @@ def test_decode3_matches_oracle(cuda):
 
 # ----------------------------------------------- full-size BASELINE configs
 
+def test_config1_rs32_1mib_fixture_on_gpu(cuda):
+    """BASELINE configs[0]: RS(3,2) encode of one 1 MiB stripe, the input
+    java.util.Random(0x5EED0001).nextBytes (HEC-T/Util.java:97-106), through
+    the host API (the JNI path) and a device row batch; both must reproduce
+    the committed parity SHA-256 of tests/golden/config1_rs_3_2_1mib.json."""
+    import hashlib
+    import json
+    import os
+    from oracle.java_random import random_bytes
+    torch = cuda
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "tests", "golden", "config1_rs_3_2_1mib.json")) as f:
+        cfg = json.load(f)
+    L = cfg["len"]
+    buf = random_bytes(0x5EED0001, 3 * L)
+    assert hashlib.sha256(buf).hexdigest() == cfg["input_sha256"]
+    rows = [np.frombuffer(buf[i * L:(i + 1) * L], dtype=np.uint8).copy() for i in range(3)]
+    code = HipReedSolomonCode(3, 2, device=0, zero_inputs_after_encode=False)
+    par = [np.zeros(L, np.uint8) for _ in range(2)]
+    code.encodeBulk(rows, par)
+    assert [hashlib.sha256(r.tobytes()).hexdigest() for r in par] == cfg["parity_sha256"]
+    st = torch.zeros((1, 5, L), dtype=torch.uint8, device="cuda")
+    st[0, 2:] = torch.from_numpy(np.stack(rows)).cuda()
+    device.encode_stripes(code, st)
+    host = st.cpu().numpy()
+    assert [hashlib.sha256(host[0, r].tobytes()).hexdigest() for r in range(2)] == cfg["parity_sha256"]
+
+
 def test_config2_rs63_64k_10k_stripes(cuda):
     """RS(6,3), 64 KiB cells, 10,000 stripes: full oracle compare on a seeded
     sample, plus every stripe checked through decode round trips."""

@@ -1,0 +1,63 @@
+"""The JNI boundary (lambdafs_amd/jni/hrs_jni.c -> lambdafs_amd/libhrs_jni.so),
+compiled against the hand-declared JNI ABI subset (jni_min.h) and driven by a
+fake JVM (tests/cpp/jni_harness.c) that enforces the JNI rules a real JVM
+checks only under -Xcheck:jni (no calls inside critical regions, none with an
+exception pending except the allowed ones, local-reference capacity, every
+frame popped, every pinned array released) and puts a guard page behind every
+byte[] so an access past a Java array faults.
+
+The precedent is libhadoop's ISA-L shim (NEC/jni_rs_encoder.c:45-63,
+NEC/jni_common.c:72-114) under NativeReedSolomonCode
+(HEC/NativeReedSolomonCode.java:55-152)."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "tests", "cpp", "jni_harness")
+SHIM = os.path.join(ROOT, "lambdafs_amd", "libhrs_jni.so")
+
+
+def run(mode, timeout=300):
+    if not os.path.exists(HARNESS):
+        subprocess.check_call(["make", "-C", ROOT, "tests/cpp/jni_harness"])
+    out = subprocess.run([HARNESS, mode], capture_output=True, text=True, timeout=timeout)
+    assert out.stdout.strip(), f"harness died: rc={out.returncode} stderr={out.stderr[-2000:]}"
+    return out.returncode, json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_shim_exports_every_native_method():
+    """Every `native` method of HrsNative.java has its JNI symbol in the shim."""
+    if not os.path.exists(SHIM):
+        subprocess.check_call(["make", "-C", ROOT, "lambdafs_amd/libhrs_jni.so"])
+    src = open(os.path.join(ROOT, "lambdafs_amd", "jni", "HrsNative.java")).read()
+    names = re.findall(r"static native \S+ (\w+)\(", src)
+    assert {"create", "createSrc", "destroy", "locationsToRead", "encode", "decode", "decode3", "encodeCrc",
+            "decodeCrc"} <= set(names)
+    lib = ctypes.CDLL(SHIM)
+    for n in names:  # JNI name mangling: '_' in the package becomes '_1'
+        getattr(lib, "Java_io_hops_erasure_1coding_HrsNative_" + n)
+
+
+def test_jni_argument_and_error_mapping():
+    """Host-only handle: NPE / IAE / AIOOBE / ISE / TooManyErasedLocations /
+    IOException exactly where the Java codec would throw, short rows rejected
+    before any row is pinned, and no JNI rule broken on any path."""
+    rc, res = run("--cpu")
+    assert rc == 0 and res["ok"], res
+    assert res["jni_rule_violations"] == 0 and res["checks"] >= 35
+
+
+@pytest.mark.gpu
+def test_jni_bit_exact_on_gpu(cuda):
+    """HrsNative.encode / decode / decode3 / encodeCrc / decodeCrc at RS(10,4)
+    with 1 MiB cells vs the oracle (non-codeword decode inputs, zlib CRCs
+    continued from running values), short rows on a live handle (AIOOBE,
+    outputs untouched, guard pages intact), and the xor / nrs / src codes."""
+    rc, res = run("--gpu")
+    assert rc == 0 and res["ok"], res
+    assert res["jni_rule_violations"] == 0

@@ -171,6 +171,44 @@ def test_src_bulk_host_rows_vs_oracle(cuda, k, p, s):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,p,s", [(10, 4, 1), (6, 3, 1), (12, 4, 1), (3, 2, 1), (10, 4, 2)])
+def test_src_encode_at_compiled_rs_shapes(cuda, k, p, s):
+    """SRC shares (k, p) with the compiled-in RS encode kernels; its G (XOR
+    groups over RS(k, r)) must never take them (the static kernel
+    used to run for any non-XOR code). Host rows, device batches and the
+    encode + CRC path, vs the oracle, at window-multiple lengths plus a tail."""
+    torch = cuda
+    import zlib
+    code = HipSimpleRegeneratingCode(k, p, s, device=0)
+    assert code.srcLayout()[0] >= 1
+    rng = np.random.default_rng(100 * k + 10 * p + s)
+    L = (64 << 10) + 77
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    want = C.src_encode_bulk(k, p, s, data)
+    par = [np.zeros(L, np.uint8) for _ in range(p)]
+    code.encodeBulk(data, par)
+    assert all((a == b).all() for a, b in zip(par, want))
+    crcs = code.encodeBulkCrc(data, [np.zeros(L, np.uint8) for _ in range(p)])
+    assert crcs == [zlib.crc32(r.tobytes()) for r in data] + [zlib.crc32(r.tobytes()) for r in want]
+    S, Ld = 3, 64 << 10  # a multiple of the fused kernel's 32 KiB window
+    st = torch.randint(0, 256, (S, k + p, Ld), dtype=torch.uint8, device="cuda")
+    device.encode_stripes(code, st)
+    host = st.cpu().numpy()
+    for i in range(S):
+        ref = C.src_encode_bulk(k, p, s, [host[i, p + c] for c in range(k)])
+        assert all((host[i, r] == ref[r]).all() for r in range(p)), i
+    code.setKernelMode(3)  # the fused encode + CRC whenever the shape allows
+    st2 = st.clone()
+    st2[:, :p] = 0
+    crc_dev = device.encode_stripes_crc(code, st2)
+    assert torch.equal(st2, st)
+    host_crc = crc_dev.cpu().numpy().view(np.uint32).reshape(S, k + p)
+    for i in range(S):
+        rows = [host[i, p + c] for c in range(k)] + [host[i, r] for r in range(p)]
+        assert [int(x) for x in host_crc[i]] == [zlib.crc32(r.tobytes()) for r in rows]
+
+
+@pytest.mark.gpu
 def test_src_every_pattern_round_trip_device(cuda):
     torch = cuda
     k, p, s = 10, 6, 2
