@@ -29,6 +29,8 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import synth  # noqa: E402  (SURVEY §8(d) synthetic stripes: splitmix64 per global stripe)
 from lambdafs_amd import HipReedSolomonCode, device, parallel  # noqa: E402
 
 GiB = float(1 << 30)
@@ -46,7 +48,10 @@ def parse():
     ap.add_argument("--cell", type=int, default=1 << 20, help="cell bytes (bufSize)")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--p", type=int, default=4)
-    ap.add_argument("--cpu-stripes", type=int, default=128, help="stripes in the CPU baseline sample")
+    ap.add_argument("--cpu-stripes", type=int, default=0,
+                    help="stripes in the CPU baseline sample (0: 8 per thread)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the config-5 end-to-end (host memory) leg")
+    ap.add_argument("--no-sha", action="store_true", help="skip the per-rank parity SHA-256")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a sample against the oracle after timing")
     ap.add_argument("--dist-backend", default="nccl",
@@ -69,19 +74,45 @@ def setup_dist(args):
     return world, rank, local
 
 
+def host_cpus():
+    """CPUs this process may use: its affinity set (what `nproc` prints),
+    capped by a cgroup CPU quota when one is set (the GPU boxes give one GPU's
+    job a share of a larger machine), plus the CPU model string."""
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return nproc, quota, model
+
+
 def cpu_baseline(k, p, L, nstripes, threads=None):
     """Restated reference CPU path (oracle/: C transcription of
     ReedSolomonCode.encodeBulk + per-byte decodeBulk 5-arg) on a bounded
-    sample of the same workload, stripes spread over host threads."""
+    sample of the same workload (the same synthetic stripes, global indices
+    3..), stripes spread over host threads."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import rs_oracle as C
     C.lib()
     n = k + p
-    cores = threads or max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
-                                  else os.cpu_count()))
-    rng = np.random.default_rng(0x5EED0003)
-    data = [[rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] for _ in range(min(nstripes, cores))]
+    nproc, quota, model = host_cpus()
+    cores = threads or min(nproc, quota or nproc)
+    nstripes = nstripes or 8 * cores
+    data = [list(synth.stripe_numpy(3, synth.EDGE_STRIPES + i, k, L)) for i in range(min(nstripes, cores))]
     erased = [p]
     to_read = sorted(C.locations_to_read(k, p, erased))
     ntr = [x for x in range(n) if x not in to_read]
@@ -107,9 +138,107 @@ def cpu_baseline(k, p, L, nstripes, threads=None):
         "unit": "GiB/s",
         "cores": cores,
         "kind": "port",
+        "nproc": nproc,
+        "cgroup_cpu_quota": quota,
+        "cpu_model": model,
         "sample": f"{nstripes} stripes RS({k},{p}) x {L >> 10} KiB cells, encode + 1-erasure decode, "
-                  f"{cores} threads, {dt:.1f} s wall",
+                  f"{cores} threads (nproc {nproc}, cgroup quota {quota or 'none'} CPUs), {dt:.1f} s wall",
     }
+
+
+def e2e_config5(local, rank, world, S=512, L=256 << 10, reps=3):
+    """BASELINE configs[4] end to end through the product's host batch API
+    (hrs_decode_batch_host): RS(12,4), 256 KiB cells, S stripes per GPU (4,096
+    over 8), a seeded random PAIR of lost locations per stripe (keyed by the
+    global stripe index), the stripes in pinned host memory; only each
+    stripe's 12 survivors cross PCIe H2D, only the 2 repaired cells come back.
+    Also the same path staged from pageable memory, and the host batch encode
+    (hrs_encode_batch_host: 12 data cells H2D, 4 parity cells D2H)."""
+    import torch
+    k, p = 12, 4
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=local)
+    dev = f"cuda:{local}"
+    g0 = rank * S
+    st_dev = torch.zeros((S, n, L), dtype=torch.uint8, device=dev)
+    synth.fill_data_rows(torch, st_dev, 5, g0, k, p)
+    st = torch.empty((S, n, L), dtype=torch.uint8, pin_memory=True)
+    st.copy_(st_dev)
+    st[:, :p] = 0
+    device.encode_stripes(code, st_dev)  # device-resident parity, to check the host batch encode
+    torch.cuda.synchronize()
+    stn = st.numpy()
+
+    def timed(fn):
+        fn()
+        ms = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ms.append((time.perf_counter() - t0) * 1e3)
+        return ms
+
+    enc_ms = timed(lambda: device.encode_batch_host(code, stn))
+    enc_ok = bool(torch.equal(st, st_dev.cpu()))
+    er = np.full((S, 2), -1, dtype=np.int32)
+    for s in range(S):
+        er[s] = np.sort(np.random.default_rng([0x5EED0005, g0 + s]).choice(n, 2, replace=False))
+    out = torch.empty((S, 2, L), dtype=torch.uint8, pin_memory=True)
+    outn = out.numpy()
+    dec_ms = timed(lambda: device.decode_batch_host(code, stn, er, outn))
+    idx = np.arange(S)[:, None]
+    dec_ok = bool(np.array_equal(outn, stn[idx, er]))
+    # pageable host memory: the same call stages through pinned slots
+    pg = np.array(stn)
+    pout = np.zeros((S, 2, L), np.uint8)
+    pg_ms = timed(lambda: device.decode_batch_host(code, pg, er, pout))
+    pg_ok = bool(np.array_equal(pout, pg[idx, er]))
+    # the link's own rate for the same survivor bytes: one pinned H2D copy
+    nbytes = k * L * S
+    src = st.view(-1)[:nbytes]
+    dst = st_dev.view(-1)[:nbytes]
+    h2d_ms = timed(lambda: (dst.copy_(src, non_blocking=True), torch.cuda.synchronize()))
+    del st_dev, dst
+    torch.cuda.empty_cache()
+    t_dec = parallel.max_over_ranks(float(np.median(dec_ms)), dev)
+    t_enc = parallel.max_over_ranks(float(np.median(enc_ms)), dev)
+    t_pg = parallel.max_over_ranks(float(np.median(pg_ms)), dev)
+    ok = parallel.all_ok(enc_ok and dec_ok and pg_ok, dev)
+    user = k * L * S * world
+
+    def rate(t_ms, nbytes):
+        return round(nbytes / GiB / (t_ms * 1e-3), 3)
+
+    return {
+        "what": "configs[4] end-to-end from host memory through hrs_decode_batch_host: RS(12,4) 256 KiB cells, "
+                f"{S} stripes/GPU, seeded random lost pair per stripe; pinned host stripes, survivors H2D, "
+                "repaired cells D2H, pipelined chunks",
+        "decode_ms": stats(dec_ms),
+        "decode_GiBps_user": rate(t_dec, user),
+        "decode_pcie_GBps": round((k + 2) * L * S * world / 1e9 / (t_dec * 1e-3), 2),
+        "h2d_peak_GBps": round(nbytes / 1e9 / (float(np.median(h2d_ms)) * 1e-3), 2),
+        "h2d_peak_how": "one pinned-host to device copy of the same 12 * 256 KiB * S survivor bytes",
+        "decode_pageable_ms": stats(pg_ms),
+        "decode_pageable_GiBps_user": rate(t_pg, user),
+        "encode_ms": stats(enc_ms),
+        "encode_GiBps_user": rate(t_enc, user),
+        "encode_pcie_GBps": round((k + p) * L * S * world / 1e9 / (t_enc * 1e-3), 2),
+        "bit_exact": ok,
+        "n_gpus": world,
+    }
+
+
+def parity_sha256(stripes, p, g0, chunk=64):
+    """SHA-256 over this rank's parity rows, stripe by stripe in global order
+    (rows 0..p-1, L bytes each); with the per-global-stripe inputs, an N-GPU
+    run's rank r must print the same digest for the same stripe range as any
+    other run covering it."""
+    import hashlib
+    h = hashlib.sha256()
+    S = stripes.shape[0]
+    for s0 in range(0, S, chunk):
+        h.update(stripes[s0:s0 + chunk, :p].contiguous().cpu().numpy().tobytes())
+    return {"first_stripe": g0, "stripes": S, "sha256": h.hexdigest()}
 
 
 def copy_peak(dev, code, nbytes=4 << 30, reps=5):
@@ -194,10 +323,12 @@ def main():
     D = parallel.broadcast_matrix(code.decodeMatrix(erased, ntr), dev)
     D_live = np.ascontiguousarray(D[:, to_read])
 
-    # synthetic stripes, resident in HBM before timing: [S, n, L] hops order
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0x5EED0003 + rank)
-    stripes = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device=dev, generator=gen)
+    # synthetic stripes, resident in HBM before timing: [S, n, L] hops order;
+    # data rows = splitmix64 keyed by (config 3, GLOBAL stripe index) with the
+    # edge stripes (all-0x00, all-0xFF, ramp) at global 0..2
+    g0 = (parallel.stripe_range(args.stripes, world, rank)[0] if args.strong else rank * S)
+    stripes = torch.zeros((S, n, L), dtype=torch.uint8, device=dev)
+    synth.fill_data_rows(torch, stripes, 3, g0, k, p)
     out = torch.empty((S, len(erased), L), dtype=torch.uint8, device=dev)
     in_rows = [stripes[:, loc, :] for loc in to_read]
     out_rows = [out[:, 0, :]]
@@ -233,11 +364,14 @@ def main():
 
     # correctness of what was timed: the decode must reproduce data shard 0
     ok = bool(torch.equal(out[:, 0], stripes[:, p]))
+    ok &= bool(torch.equal(stripes[min(S - 1, S // 2), p:].cpu(),
+                           torch.from_numpy(synth.stripe_numpy(3, g0 + min(S - 1, S // 2), k, L))))
     if args.check:
         from oracle import rs_oracle as C
-        host = stripes[S // 2].cpu().numpy()
-        ref = np.stack(C.encode_bulk(k, p, [host[p + c] for c in range(k)]))
-        ok &= bool((host[:p] == ref).all())
+        for s_chk in sorted({0, S // 2, S - 1}):
+            host = stripes[s_chk].cpu().numpy()
+            ref = np.stack(C.encode_bulk(k, p, [host[p + c] for c in range(k)]))
+            ok &= bool((host[:p] == ref).all())
     if not parallel.all_ok(ok, dev):
         raise RuntimeError("benchmark output failed its round-trip check")
 
@@ -288,6 +422,21 @@ def main():
     fused_ms = med_ms(lambda: device.encode_stripes_crc(code, stripes), reps)
     two_ms = med_ms(lambda: (device.encode_stripes(code, stripes), device.crc32_rows(code, cells)), reps)
 
+    sha = None
+    if not args.no_sha:
+        mine = parity_sha256(stripes, p, g0)
+        if world > 1:
+            allv = [None] * world
+            dist.all_gather_object(allv, mine)
+            sha = allv
+        else:
+            sha = [mine]
+    e2e = None
+    if not args.no_e2e:
+        del cells
+        torch.cuda.empty_cache()
+        e2e = e2e_config5(local, rank, world)
+
     total_stripes = args.stripes if args.strong else S * world
     user_bytes = 2 * k * L * total_stripes * args.steps
     enc_bytes = (k + p) * L * S  # algorithmic bytes per encode launch (read k, write p)
@@ -310,7 +459,8 @@ def main():
             "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (torch.randint uniform bytes, seeded per rank)",
+            "data": "synthetic: splitmix64 per global stripe (base seed 0x5EED0003), edge stripes "
+                    "0x00/0xFF/ramp at global 0..2 (SURVEY §8d)",
             "config": {
                 "workload": f"RS({k},{p}) encode + 1-erasure decode (data shard 0), {L >> 10} KiB cells, "
                             f"{S} stripes/GPU, device-resident",
@@ -358,11 +508,14 @@ def main():
                 "speedup_vs_two_pass": round(float(np.median(two_ms)) / float(np.median(fused_ms)), 3),
             },
             "copy_peak": peak,
+            "parity_sha256": sha,
+            "e2e_config5": e2e,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
             res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 12, threads=1)
+            res["cpu_baseline"]["gpu_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

@@ -225,6 +225,36 @@ hrs_status hrs_decode_batch_dev(hrs_codec* codec, const uint8_t* stripes, size_t
                                 size_t out_row_stride, size_t out_stripe_stride, size_t len,
                                 size_t nstripes, void* stream);
 
+/* ---- host-memory batches: many stripes per call, pipelined ----
+ * Stripes start and end in host memory (DataNode sockets / local block files;
+ * Encoder.encodeFile over a file's stripes, Encoder.java:289-382; a repair job
+ * over many stripes, BlockReconstructor -> Decoder.fixErasedBlockImpl per
+ * stripe, Decoder.java:232-401). The stripes flow in chunks through a ring of
+ * device slots, each on its own stream: H2D of exactly the rows the chunk's
+ * code reads, the kernel, D2H of exactly the rows it writes, successive chunks
+ * overlapping. Buffers allocated pinned (hipHostMalloc, hipHostRegister, torch
+ * pin_memory) are DMA'd directly and the whole job is queued at once;
+ * pageable buffers are staged through the handle's pinned slots by the copy
+ * pool. Synchronous: outputs are in place when the call returns. Rows need no
+ * alignment. */
+
+/* hrs_decode_batch_dev over host memory (same layout, semantics and errors):
+ * stripe s holds location l at stripes + s * stripe_stride + l * row_stride;
+ * only the survivors each stripe's pattern reads cross PCIe (k of the n for
+ * rs; fewer for src local groups), and output t of stripe s lands at
+ * out + s * out_stripe_stride + t * out_row_stride. */
+hrs_status hrs_decode_batch_host(hrs_codec* codec, const uint8_t* stripes, size_t row_stride,
+                                 size_t stripe_stride, const int* erased, int max_erased, uint8_t* out,
+                                 size_t out_row_stride, size_t out_stripe_stride, size_t len,
+                                 size_t nstripes);
+
+/* encodeBulk of every stripe of a host batch, in place: reads data rows
+ * (hops locations p..n-1) and writes parity rows (locations 0..p-1) of stripe
+ * s at stripes + s * stripe_stride + l * row_stride. Only the k data rows go
+ * H2D and the p parity rows D2H. */
+hrs_status hrs_encode_batch_host(hrs_codec* codec, uint8_t* stripes, size_t row_stride, size_t stripe_stride,
+                                 size_t len, size_t nstripes);
+
 /* Generic GF(2^8) matrix x rows: out_o = XOR_i m[o * nin + i] * in_i (m on
  * the host, row-major nout x nin). Used with coding matrices broadcast over
  * RCCL, and by the 3-arg decode. nin, nout in [1, 255]. */

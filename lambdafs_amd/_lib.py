@@ -35,7 +35,7 @@ EXPORTS = (
     "hrs_locations_to_read", "hrs_encode_matrix", "hrs_decode_matrix",
     "hrs_encode", "hrs_decode", "hrs_decode3", "hrs_encode_crc", "hrs_decode_crc",
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
-    "hrs_encode_crc_dev",
+    "hrs_encode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_set_kernel_mode",
 )
 
@@ -95,6 +95,8 @@ def lib():
         "hrs_apply_dev": ([P, U8P, I, I, PP, S, PP, S, S, S, P], I),
         "hrs_crc32_dev": ([P, PP, I, S, S, S, P, P, P], I),
         "hrs_encode_crc_dev": ([P, PP, S, PP, S, S, S, P, P, P], I),
+        "hrs_decode_batch_host": ([P, P, S, S, P, I, P, S, S, S, S], I),
+        "hrs_encode_batch_host": ([P, P, S, S, S, S], I),
         "hrs_set_kernel_mode": ([P, I], I),
     }
     for name, (args, res) in sigs.items():

@@ -61,6 +61,7 @@ int device_cu_count();  // CUs of the current device (cached)
 // ---- heterogeneous batches: one erasure pattern per stripe (hrs_decode_batch_dev)
 
 constexpr int kBatchMaxIn = 16;
+constexpr int kHostBatchSlots = 3;  // chunk slots of the host-memory batch pipeline
 struct BatchPlan {            // one erasure pattern, a device table entry
   int nin;                    // live survivor rows read
   int nout;                   // erased rows written

@@ -121,6 +121,49 @@ def decode_batch(code, stripes, erased, out):
         out.data_ptr(), out.stride(1), out.stride(0), L, S, _stream(stripes)))
 
 
+def _host_ptr(a, name, writable=False):
+    """Base address of a host batch (numpy array or CPU tensor, pinned or not)."""
+    torch = _lib.torch
+    if torch is not None and isinstance(a, torch.Tensor):
+        if a.is_cuda or a.dtype != torch.uint8:
+            raise ValueError(f"{name} must be a host uint8 tensor")
+        return a.data_ptr(), tuple(a.shape), tuple(a.stride())
+    a = np.asarray(a)
+    if a.dtype != np.uint8 or (writable and not a.flags["WRITEABLE"]):
+        raise ValueError(f"{name} must be a {'writable ' if writable else ''}uint8 array")
+    return a.ctypes.data, a.shape, tuple(x // a.itemsize for x in a.strides)
+
+
+def decode_batch_host(code, stripes, erased, out):
+    """hrs_decode_batch_host: decode_batch for stripes[S, n, L] and out[S, E, L]
+    in HOST memory (numpy arrays or CPU tensors; pinned ones are DMA'd
+    directly). Only each stripe's survivors go over PCIe, only the repaired
+    cells come back; chunks of stripes pipeline through the device."""
+    n = code.stripeSize() + code.paritySize()
+    sp, sshape, sstr = _host_ptr(stripes, "stripes")
+    op, oshape, ostr = _host_ptr(out, "out", writable=True)
+    e = np.ascontiguousarray(np.asarray(erased, dtype=np.int32))
+    if len(sshape) != 3 or sshape[1] != n or sstr[2] != 1:
+        raise ValueError(f"stripes must be [S, {n}, L] with unit byte stride")
+    S, L = sshape[0], sshape[2]
+    if e.ndim != 2 or e.shape[0] != S:
+        raise ValueError("erased must be [S, E]")
+    if len(oshape) != 3 or tuple(oshape) != (S, e.shape[1], L) or ostr[2] != 1:
+        raise ValueError("out must be [S, E, L]")
+    code._check(_lib.lib().hrs_decode_batch_host(
+        code._handle(), sp, sstr[1], sstr[0], e.ctypes.data, e.shape[1], op, ostr[1], ostr[0], L, S))
+
+
+def encode_batch_host(code, stripes):
+    """hrs_encode_batch_host: parity rows of every stripe of a HOST batch
+    stripes[S, n, L] (hops order) from its data rows, in place."""
+    n = code.stripeSize() + code.paritySize()
+    sp, sshape, sstr = _host_ptr(stripes, "stripes", writable=True)
+    if len(sshape) != 3 or sshape[1] != n or sstr[2] != 1:
+        raise ValueError(f"stripes must be [S, {n}, L] with unit byte stride")
+    code._check(_lib.lib().hrs_encode_batch_host(code._handle(), sp, sstr[1], sstr[0], sshape[2], sshape[0]))
+
+
 def apply_rows(code, matrix, in_rows, out_rows):
     """out_o = XOR_i matrix[o, i] * in_i over S stripes (matrix: host uint8 [nout, nin]).
     Used with coding matrices broadcast over RCCL (bench.py --gpus N)."""
