@@ -12,7 +12,7 @@ HDRS     := include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf2
             lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
 
 JNI      := lambdafs_amd/libhrs_jni.so
-HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness
+HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic
 
 all: $(LIB) $(ORACLE) $(JNI) $(HARNESS)
 
@@ -28,9 +28,12 @@ build/hrs_crc.o: lambdafs_amd/csrc/hrs_crc.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# The fused kernels' XOR networks and CRC steps must unroll completely (a
+# K = 12 network otherwise stays a loop of runtime mask tests, 5x slower):
+# lift the pragma-unroll size cap for this file.
 build/hrs_fused.o: lambdafs_amd/csrc/hrs_fused.hip $(HDRS)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -mllvm -pragma-unroll-threshold=1000000 -c $< -o $@
 
 $(LIB): build/hrs_api.o build/hrs_kernels.o build/hrs_crc.o build/hrs_fused.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
@@ -54,10 +57,63 @@ tests/cpp/jni_harness: tests/cpp/jni_harness.c lambdafs_amd/jni/jni_min.h $(JNI)
 	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs_jni -lhrs -Loracle -loracle -lz \
 	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
+# Host-only logic (matrices, survivor lists, decode cache, batch plans) vs the oracle.
+tests/cpp/host_logic: tests/cpp/host_logic.cpp include/hrs.h $(LIB) $(ORACLE)
+	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs -Loracle -loracle \
+	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
 tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
 	g++ -O2 -std=c++17 -Wall -o $@ $< -lz
+
+# ---- make asan: the host-side code under AddressSanitizer + UBSan (clang,
+# one runtime for all): libhrs's host logic (hrs_api.cpp, host code only: -Xarch_host),
+# the oracle, the JNI shim, and the CPU drivers of each (host-only handles,
+# the fake JVM). GPU kernels are not instrumented (no GPU ASan on this pool).
+# Logs: profiles/r02/asan/.
+ASAN_DIR := build/asan
+CLANG    := /opt/rocm/lib/llvm/bin/clang
+SAN      := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+HSAN     := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
+            -Xarch_host -fno-omit-frame-pointer
+ASAN_BIN := $(ASAN_DIR)/host_logic $(ASAN_DIR)/jni_harness $(ASAN_DIR)/codec_harness
+ASAN_LOG := profiles/r02/asan
+
+$(ASAN_DIR)/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS) lambdafs_amd/csrc/hrs_host.hpp
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) $(HSAN) -x hip -c $< -o $@
+
+$(ASAN_DIR)/libhrs.so: $(ASAN_DIR)/hrs_api.o build/hrs_kernels.o build/hrs_crc.o build/hrs_fused.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -fsanitize=address,undefined -o $@ $^
+
+$(ASAN_DIR)/liboracle.so: oracle/rs_oracle.c oracle/rs_oracle.h
+	@mkdir -p $(ASAN_DIR)
+	$(CLANG) $(SAN) -std=c11 -fPIC -shared -o $@ oracle/rs_oracle.c
+
+$(ASAN_DIR)/libhrs_jni.so: lambdafs_amd/jni/hrs_jni.c lambdafs_amd/jni/jni_min.h include/hrs.h $(ASAN_DIR)/libhrs.so
+	$(CLANG) $(SAN) -std=c11 -fPIC -shared -Iinclude -o $@ $< -L$(ASAN_DIR) -lhrs
+
+ASAN_RPATH := -Wl,-rpath,'$$ORIGIN'
+$(ASAN_DIR)/host_logic: tests/cpp/host_logic.cpp $(ASAN_DIR)/libhrs.so $(ASAN_DIR)/liboracle.so
+	$(CLANG)++ $(SAN) -std=c++17 -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs -loracle $(ASAN_RPATH)
+
+$(ASAN_DIR)/jni_harness: tests/cpp/jni_harness.c $(ASAN_DIR)/libhrs_jni.so $(ASAN_DIR)/liboracle.so
+	$(CLANG) $(SAN) -std=c11 -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs_jni -lhrs -loracle -lz $(ASAN_RPATH)
+
+$(ASAN_DIR)/codec_harness: tests/cpp/codec_harness.cpp include/hrs.hpp $(ASAN_DIR)/libhrs.so $(ASAN_DIR)/liboracle.so
+	$(CLANG)++ $(SAN) -std=c++17 -pthread -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs -loracle -lz $(ASAN_RPATH)
+
+asan: $(ASAN_BIN)
+	@mkdir -p $(ASAN_LOG)
+	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 LSAN_OPTIONS=suppressions=tools/lsan.supp \
+	UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 sh -c '\
+	  set -e; \
+	  $(ASAN_DIR)/host_logic; \
+	  $(ASAN_DIR)/jni_harness --cpu; \
+	  for kp in "10 4" "12 4" "6 3" "3 2"; do $(ASAN_DIR)/codec_harness --host-only $$kp; done' \
+	  > $(ASAN_LOG)/asan_run.log 2>&1 || { cat $(ASAN_LOG)/asan_run.log; exit 1; }
+	@cat $(ASAN_LOG)/asan_run.log
 
 clean:
 	rm -rf build $(LIB) $(ORACLE) $(JNI) $(HARNESS)
 
-.PHONY: all clean
+.PHONY: all clean asan

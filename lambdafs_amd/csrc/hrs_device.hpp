@@ -85,6 +85,33 @@ __device__ __forceinline__ void store_row(uint8_t* p, int lane, const uint32_t (
   __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(p + 1024 + lane * 16));
 }
 
+// Same accesses from a wave-uniform row base plus the lane's 32-bit byte
+// offset (16 * lane): the compiler can then address with an SGPR base and one
+// shared VGPR offset (global_load ... v_off, s[base]) instead of a 64-bit
+// VGPR address per row, which in register-tight kernels it would spill.
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ void load_row_u(const uint8_t* base, uint32_t loff, uint32_t (&w)[8]) {
+  const uint8_t* b = uniform_ptr(base);
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b + loff));
+  const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b + loff + 1024u));
+  w[0] = x[0]; w[1] = x[1]; w[2] = x[2]; w[3] = x[3];
+  w[4] = y[0]; w[5] = y[1]; w[6] = y[2]; w[7] = y[3];
+}
+
+__device__ __forceinline__ void store_row_u(uint8_t* base, uint32_t loff, const uint32_t (&w)[8]) {
+  uint8_t* b = const_cast<uint8_t*>(uniform_ptr(base));
+  const u32x4 x = {w[0], w[1], w[2], w[3]};
+  const u32x4 y = {w[4], w[5], w[6], w[7]};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(b + loff));
+  __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(b + loff + 1024u));
+}
+
 __device__ __forceinline__ uint32_t wave_id_in_grid() {
   return __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
 }

@@ -21,6 +21,18 @@ def run(*args, timeout=600):
     return out.returncode, json.loads(line)
 
 
+def test_host_logic_vs_oracle():
+    """tests/cpp/host_logic.cpp through host-only handles: every code family's
+    matrices and survivor lists vs the oracle, the decode cache past its
+    eviction bound, batch plans, argument errors (also the `make asan` run)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "host_logic")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", ROOT, "tests/cpp/host_logic"])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and res["ok"], res
+
+
 @pytest.mark.parametrize("k,p", [(10, 4), (12, 4), (6, 3), (3, 2)])
 def test_harness_host_only(k, p):
     rc, res = run("--host-only", k, p)
