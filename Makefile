@@ -8,7 +8,7 @@ CC       ?= gcc
 
 LIB      := lambdafs_amd/libhrs.so
 ORACLE   := oracle/liboracle.so
-HDRS     := include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
+HDRS     := Makefile include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
             lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
 
 JNI      := lambdafs_amd/libhrs_jni.so

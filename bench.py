@@ -501,7 +501,7 @@ def main():
             },
             "encode_crc": {
                 "what": "encode + java.util.zip.CRC32 of all k+p cells (Encoder with computeBlockChecksum)",
-                "kernel": f"encode_crc_kernel<{k},{p}> + crc_fold_kernel",
+                "kernel": f"encode_crc_grouped_kernel<{k},{p},G=2> + crc_fold_kernel",
                 "fused_ms": stats(fused_ms),
                 "two_pass_ms": stats(two_ms),
                 "fused_GBps_algorithmic": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9, 1),

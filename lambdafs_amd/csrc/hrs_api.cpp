@@ -861,18 +861,25 @@ hrs_status upload(hrs_codec* c, const std::vector<uint32_t>& h, uint32_t** out) 
   return HRS_OK;
 }
 
-hrs_status crc_window_tables(hrs_codec* c) {
-  if (c->crc_tables_a) return HRS_OK;
+// The LDS image of the window kernels (crc_window_kernel, the fused encode +
+// CRC): slicing tables (32 bank-private copies), then Z_chunk (joins a lane's
+// successive pieces, `chunk` bytes apart) and the lane tree Z_{piece * 2^t}
+// (lane l + 2^t is piece * 2^t bytes later).
+hrs_status crc_image(hrs_codec* c, uint64_t piece, uint64_t chunk, uint32_t** out) {
+  if (*out) return HRS_OK;
   namespace cr = hrs::crc;
   std::vector<uint32_t> h(hrs::kCrcLdsWordsA);
   const cr::Slice4 sl = cr::make_slice4();
   for (int j = 0; j < 4; ++j)
     for (int v = 0; v < 256; ++v)
       for (int r = 0; r < hrs::kCrcRep; ++r) h[hrs::crc_slice_word(j, v, r)] = sl.s[j].t[v];
-  cr::to_tables(cr::zeros(cr::kChunkBytes), &h[hrs::kCrcSliceWords]);  // joins a lane's pieces, chunk to chunk
-  for (int t = 0; t < 6; ++t)  // lane tree: lane l + 2^t is 16 * 2^t bytes later
-    cr::to_tables(cr::zeros(static_cast<uint64_t>(cr::kPieceBytes) << t), &h[hrs::kCrcSliceWords + (1 + t) * 1024]);
-  return upload(c, h, &c->crc_tables_a);
+  cr::to_tables(cr::zeros(chunk), &h[hrs::kCrcSliceWords]);
+  for (int t = 0; t < 6; ++t) cr::to_tables(cr::zeros(piece << t), &h[hrs::kCrcSliceWords + (1 + t) * 1024]);
+  return upload(c, h, out);
+}
+
+hrs_status crc_window_tables(hrs_codec* c) {
+  return crc_image(c, hrs::crc::kPieceBytes, hrs::crc::kChunkBytes, &c->crc_tables_a);
 }
 
 hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, const uint32_t** out) {

@@ -89,27 +89,32 @@ __device__ __forceinline__ void store_row(uint8_t* p, int lane, const uint32_t (
 // offset (16 * lane): the compiler can then address with an SGPR base and one
 // shared VGPR offset (global_load ... v_off, s[base]) instead of a 64-bit
 // VGPR address per row, which in register-tight kernels it would spill.
-__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+// (The pointers are rebuilt in the global address space: a plain cast back
+// from integers would make them flat accesses, which also count in lgkmcnt
+// and so stall every LDS wait behind the row loads.)
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+__device__ __forceinline__ uint64_t uniform_addr(const void* p) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
-  return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
 __device__ __forceinline__ void load_row_u(const uint8_t* base, uint32_t loff, uint32_t (&w)[8]) {
-  const uint8_t* b = uniform_ptr(base);
-  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b + loff));
-  const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b + loff + 1024u));
+  const g_u32x4* b = reinterpret_cast<const g_u32x4*>(uniform_addr(base) + loff);
+  const u32x4 x = __builtin_nontemporal_load(b);
+  const u32x4 y = __builtin_nontemporal_load(b + 64);  // + 1024 bytes
   w[0] = x[0]; w[1] = x[1]; w[2] = x[2]; w[3] = x[3];
   w[4] = y[0]; w[5] = y[1]; w[6] = y[2]; w[7] = y[3];
 }
 
 __device__ __forceinline__ void store_row_u(uint8_t* base, uint32_t loff, const uint32_t (&w)[8]) {
-  uint8_t* b = const_cast<uint8_t*>(uniform_ptr(base));
+  g_u32x4* b = reinterpret_cast<g_u32x4*>(uniform_addr(base) + loff);
   const u32x4 x = {w[0], w[1], w[2], w[3]};
   const u32x4 y = {w[4], w[5], w[6], w[7]};
-  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(b + loff));
-  __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(b + loff + 1024u));
+  __builtin_nontemporal_store(x, b);
+  __builtin_nontemporal_store(y, b + 64);
 }
 
 __device__ __forceinline__ uint32_t wave_id_in_grid() {
@@ -197,12 +202,27 @@ __device__ __forceinline__ uint32_t slice4(const SliceTab& t, uint32_t x) {
   return xor3(lds_at(a3 + 128u), lds_at(a2), lds_at(a1 + 128u)) ^ lds_at(a0);
 }
 
+// slice4(t, x) ^ y in two VALU ops (the next word of the piece folds into
+// the step's own XOR tree).
+__device__ __forceinline__ uint32_t slice4_xor(const SliceTab& t, uint32_t x, uint32_t y) {
+  const uint32_t a3 = __builtin_amdgcn_perm(x, t.lw_hi, 0x0C020400u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, t.lw_hi, 0x0C020500u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, t.lw_lo, 0x0C0C0600u);
+  const uint32_t a0 = __builtin_amdgcn_perm(x, t.lw_lo, 0x0C0C0700u);
+  return xor3(xor3(lds_at(a3 + 128u), lds_at(a2), lds_at(a1 + 128u)), lds_at(a0), y);
+}
+
 // Raw CRC of one 16-byte piece (4 little-endian words).
 __device__ __forceinline__ uint32_t piece_crc(const SliceTab& s, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-  uint32_t c = slice4(s, w0);
-  c = slice4(s, c ^ w1);
-  c = slice4(s, c ^ w2);
-  return slice4(s, c ^ w3);
+  uint32_t c = slice4_xor(s, w0, w1);
+  c = slice4_xor(s, c, w2);
+  c = slice4_xor(s, c, w3);
+  return slice4(s, c);
+}
+
+// Z(c) ^ y from a 4 x 256 table image in LDS (two VALU ops for the XORs).
+__device__ __forceinline__ uint32_t zmul_xor(const uint32_t* z, uint32_t c, uint32_t y) {
+  return xor3(xor3(z[c & 0xFFu], z[256 + ((c >> 8) & 0xFFu)], z[512 + ((c >> 16) & 0xFFu)]), z[768 + (c >> 24)], y);
 }
 
 // Raw CRCs of the lane's two pieces of M rows (row m's words x[m][0..3] and

@@ -94,159 +94,21 @@ __global__ void __launch_bounds__(THREADS) encode_crc_kernel(const EncodeCrcArgs
   }
 }
 
-// Second form (the default; HRS_FUSED=1 selects the one above for A/B):
-// the row-serial kernel above waits on every row's load before touching it
-// (one 2 KiB row in flight per wave: the ISA shows a vmcnt(0) per row), so
-// HBM latency, not bandwidth, set its pace. Here a wave loads ALL K data rows
-// of a sub-window at once (K x 8 VGPRs), CRCs them as 2K independent chains
-// advanced in lockstep (8K LDS lookups in flight per slicing step), slices
-// them, and then builds each parity row in turn straight from the planes
-// (acc[q] = XOR of the planes G selects, no cross-row pending state), storing
-// and CRC'ing it before the next. The next sub-window's K loads are issued as
-// soon as the last parity's planes are built, so they overlap that row's
-// un-slice, store and CRC chains, and the lane-tree / Horner updates.
-#ifndef HRS_CRC_GROUP
-#define HRS_CRC_GROUP 2
-#endif
-constexpr int kCrcGroup = HRS_CRC_GROUP;  // rows whose CRC chains advance together
-
-template <int K, int P, class MATRIX>
-__device__ __forceinline__ void parity_planes(int o, const uint32_t (&x)[K][8], uint32_t (&acc)[8]) {
-  constexpr StaticPlan<K, P, MATRIX> plan{};
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    uint32_t v = 0u, pend = 0u;
-    bool first = true, has = false;
-#pragma unroll
-    for (int r = 0; r < K; ++r)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if ((plan.mask[o][r][q] >> i) & 1) {
-          if (first) {
-            v = x[r][i];
-            first = false;
-          } else if (has) {
-            v = xor3(v, pend, x[r][i]);
-            has = false;
-          } else {
-            pend = x[r][i];
-            has = true;
-          }
-        }
-    acc[q] = has ? v ^ pend : v;
-  }
-}
-
-// The scheduler otherwise interleaves the phases (and the two sub-windows of
-// the unrolled pair) for ILP until the live ranges spill; a scheduling
-// barrier between phases keeps each phase's temporaries short-lived.
+// The scheduler otherwise interleaves the row groups for ILP until the live
+// ranges spill; a scheduling barrier between them keeps each group's
+// temporaries short-lived.
 #ifndef HRS_NO_PHASE_FENCE
 #define HRS_PHASE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define HRS_PHASE_FENCE() ((void)0)
 #endif
 
-// One sub-window of the second form: source CRCs of the K rows in x
-// (natural byte order), slice them, then each parity row from the planes:
-// un-slice, store, CRC. x is consumed (left sliced).
-template <int K, int P, class MATRIX>
-__device__ __forceinline__ void encode_crc_sub(uint32_t (&x)[K][8], uint32_t (&crc)[K + P], const SliceTab& slices,
-                                               const uint32_t* zchunk, const EncodeCrcArgs& a, uint64_t out_base,
-                                               int lane) {
-#pragma unroll
-  for (int r0 = 0; r0 < K; r0 += kCrcGroup) {
-    constexpr int G = kCrcGroup;
-    if (r0 + G <= K) {
-      uint32_t c0[G], c1[G];
-      rows_piece_crcs<G>(slices, *reinterpret_cast<const uint32_t(*)[G][8]>(&x[r0][0]), c0, c1);
-#pragma unroll
-      for (int g = 0; g < G; ++g) crc[r0 + g] = zmul(zchunk, zmul(zchunk, crc[r0 + g]) ^ c0[g]) ^ c1[g];
-    } else {  // the last K % G rows
-#pragma unroll
-      for (int r = r0; r < K; ++r) {
-        uint32_t d0[1], d1[1];
-        rows_piece_crcs<1>(slices, *reinterpret_cast<const uint32_t(*)[1][8]>(&x[r][0]), d0, d1);
-        crc[r] = zmul(zchunk, zmul(zchunk, crc[r]) ^ d0[0]) ^ d1[0];
-      }
-    }
-#pragma unroll
-    for (int r = r0; r < r0 + G && r < K; ++r) bitslice(x[r]);
-    HRS_PHASE_FENCE();
-  }
-#pragma unroll
-  for (int o = 0; o < P; ++o) {
-    HRS_PHASE_FENCE();
-    uint32_t acc[1][8];
-    parity_planes<K, P, MATRIX>(o, x, acc[0]);
-    bitslice(acc[0]);
-    store_row(a.out[o] + out_base, lane, acc[0]);
-    uint32_t p0[1], p1[1];
-    rows_piece_crcs<1>(slices, acc, p0, p1);
-    crc[K + o] = zmul(zchunk, zmul(zchunk, crc[K + o]) ^ p0[0]) ^ p1[0];
-  }
-}
-
-// 512 threads (8 waves, 2 per SIMD: 256 VGPRs each) so that a wave can hold
-// TWO sub-windows of rows: while it works on one, the next one's K loads are
-// in flight (software pipelining over the 16 sub-windows of its window).
-template <int K, int P, class MATRIX, int THREADS>
-__global__ void __launch_bounds__(THREADS) encode_crc2_kernel(const EncodeCrcArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  for (int i = threadIdx.x; i < kCrcLdsWordsA; i += THREADS) lds[i] = a.tables[i];
-  __syncthreads();
-  constexpr int N = K + P;
-  const int lane = threadIdx.x & 63;
-  const SliceTab slices = slice_tab(lane);
-  const uint32_t* zchunk = lds + kCrcSliceWords;
-  const uint32_t* tree = zchunk + 1024;
-  const uint64_t ntasks = a.nstripes * a.nwin;
-  const uint32_t nwaves = gridDim.x * (THREADS / 64);
-  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
-    const uint64_t stripe = t / a.nwin;
-    const uint64_t w = t - stripe * a.nwin;
-    const uint64_t in_base = stripe * a.in_stride + w * kCrcWindow;
-    const uint64_t out_base = stripe * a.out_stride + w * kCrcWindow;
-    uint32_t crc[N];
-#pragma unroll
-    for (int r = 0; r < N; ++r) crc[r] = 0u;
-    uint32_t xa[K][8], xb[K][8];
-#pragma unroll
-    for (int r = 0; r < K; ++r) load_row(a.in[r] + in_base, lane, xa[r]);
-#pragma unroll 1
-    for (int sub = 0; sub < kSubWindows; sub += 2) {
-      const uint64_t off = static_cast<uint64_t>(sub) * kWindowBytes;
-#pragma unroll
-      for (int r = 0; r < K; ++r) load_row(a.in[r] + in_base + off + kWindowBytes, lane, xb[r]);
-      encode_crc_sub<K, P, MATRIX>(xa, crc, slices, zchunk, a, out_base + off, lane);
-      if (sub + 2 < kSubWindows) {
-#pragma unroll
-        for (int r = 0; r < K; ++r) load_row(a.in[r] + in_base + off + 2 * kWindowBytes, lane, xa[r]);
-      }
-      encode_crc_sub<K, P, MATRIX>(xb, crc, slices, zchunk, a, out_base + off + kWindowBytes, lane);
-    }
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      const uint32_t c = lane_tree(tree, crc[r]);
-      if (lane == 0) a.raw[(stripe * N + r) * a.nwin + w] = c;
-    }
-  }
-}
-
-// Third form: the row-serial walk of the first (1024 threads, 4 waves per
-// SIMD, the CRC of row r overlapping other waves' work), but each wave keeps
-// D rows of loads in flight ahead of the row it is on — a ring of D + 1 row
-// buffers over the flat sequence (sub-window, row), crossing into the next
-// sub-window — instead of waiting on every row's load. The registers come
-// from dropping the first form's cross-row pending planes: a row's selected
-// planes are paired within the row (xor3), an odd one XORs alone.
-// D + 1 divides K, so each buffer index is a compile-time constant.
-// Ring sizes instantiated: every B <= 4 that divides K (B = 5 at K = 10 left
-// the ring in scratch memory); HRS_FUSED_RING picks
-// one for A/B runs (default: kDefaultRing, or the largest divisor below it).
-constexpr int kDefaultRing = 2;
-
-template <int K, int P, class MATRIX>
-__device__ __forceinline__ void encode_row_acc_local(int r, const uint32_t (&w)[8], uint32_t (&acc)[P][8]) {
+// Accumulates the sliced rows r0 .. r0+G-1 (those below K) into the parity
+// planes: each plane's selected input planes across the whole group are
+// paired into xor3s, so an odd leftover costs a lone XOR once per group
+// instead of once per row.
+template <int K, int P, class MATRIX, int G>
+__device__ __forceinline__ void encode_group_acc(int r0, const uint32_t (&x)[G][8], uint32_t (&acc)[P][8]) {
   constexpr StaticPlan<K, P, MATRIX> plan{};
 #pragma unroll
   for (int o = 0; o < P; ++o)
@@ -255,28 +117,40 @@ __device__ __forceinline__ void encode_row_acc_local(int r, const uint32_t (&w)[
       uint32_t pend = 0u;
       bool has = false;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if ((plan.mask[o][r][q] >> i) & 1) {
-          if (has) {
-            acc[o][q] = xor3(acc[o][q], pend, w[i]);
-            has = false;
-          } else {
-            pend = w[i];
-            has = true;
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (r0 + g < K && ((plan.mask[o][r0 + g < K ? r0 + g : 0][q] >> i) & 1)) {
+            if (has) {
+              acc[o][q] = xor3(acc[o][q], pend, x[g][i]);
+              has = false;
+            } else {
+              pend = x[g][i];
+              has = true;
+            }
           }
-        }
       if (has) acc[o][q] ^= pend;
     }
 }
 
-template <int K, int P, class MATRIX, int THREADS, int B>
-__global__ void __launch_bounds__(THREADS) encode_crc3_kernel(const EncodeCrcArgs a) {
-  static_assert(K % B == 0, "ring size must divide K");
+// Grouped form (the default; HRS_FUSED=1 selects the row-serial one above for
+// A/B runs). The same window walk, but the K data rows of a sub-window go in
+// groups of G: a group's G loads issue together from wave-uniform row bases
+// (SGPR base + one shared VGPR lane offset), its 2G CRC chains advance in
+// lockstep (8G independent LDS lookups per slicing step), each running CRC is
+// pinned in place as soon as it is updated (otherwise the compiler sinks its
+// final XORs to the loop end and keeps every row's table words live:
+// spills), and the group's planes are paired into xor3s across its rows (an
+// odd leftover costs one XOR per group, not per row). The next word of a
+// piece folds into each slicing step's XOR tree (slice4_xor), the Horner
+// term into the zmul's (zmul_xor). Per 2 KiB sub-window of RS(10,4): 2,313
+// VALU (row-serial: 2,473). G need not divide K (a last, smaller group).
+template <int K, int P, class MATRIX, int THREADS, int G>
+__global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const EncodeCrcArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   for (int i = threadIdx.x; i < kCrcLdsWordsA; i += THREADS) lds[i] = a.tables[i];
   __syncthreads();
   constexpr int N = K + P;
-  // B row buffers: B - 1 loads ahead
   const int lane = threadIdx.x & 63;
   const uint32_t loff = static_cast<uint32_t>(lane) * 16u;
   const SliceTab slices = slice_tab(lane);
@@ -292,9 +166,6 @@ __global__ void __launch_bounds__(THREADS) encode_crc3_kernel(const EncodeCrcArg
     uint32_t crc[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) crc[r] = 0u;
-    uint32_t ring[B][8];
-#pragma unroll
-    for (int r = 0; r < B - 1; ++r) load_row_u(a.in[r] + in_base, loff, ring[r]);
 #pragma unroll 1
     for (int sub = 0; sub < kSubWindows; ++sub) {
       const uint64_t off = static_cast<uint64_t>(sub) * kWindowBytes;
@@ -304,24 +175,42 @@ __global__ void __launch_bounds__(THREADS) encode_crc3_kernel(const EncodeCrcArg
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
 #pragma unroll
-      for (int r = 0; r < K; ++r) {
-        // keep B - 1 rows in flight: row r + B - 1 (possibly of the next sub-window)
+      for (int r0 = 0; r0 < K; r0 += G) {
         HRS_PHASE_FENCE();
-        const int ahead = r + B - 1;
-        if (ahead < K) {
-          load_row_u(a.in[ahead] + in_base + off, loff, ring[ahead % B]);
-        } else if (sub + 1 < kSubWindows) {
-          load_row_u(a.in[ahead - K] + in_base + off + kWindowBytes, loff, ring[ahead % B]);
+        uint32_t x[G][8];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (r0 + g < K) load_row_u(a.in[r0 + g] + in_base + off, loff, x[g]);
+        uint32_t c0[G], c1[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          c0[g] = x[g][0];
+          c1[g] = x[g][4];
         }
-        uint32_t(&x)[8] = ring[r % B];
-        const uint32_t c0 = piece_crc(slices, x[0], x[1], x[2], x[3]);
-        const uint32_t c1 = piece_crc(slices, x[4], x[5], x[6], x[7]);
-        crc[r] = zmul(zchunk, zmul(zchunk, crc[r]) ^ c0) ^ c1;
-        // materialize the running CRC here: otherwise its final XORs sink to
-        // the loop's end and every row's table words stay live (spills)
-        __asm__ volatile("" : "+v"(crc[r]));
-        bitslice(x);
-        encode_row_acc_local<K, P, MATRIX>(r, x, acc);
+#pragma unroll
+        for (int st = 0; st < 3; ++st)
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+            if (r0 + g < K) {
+              c0[g] = slice4_xor(slices, c0[g], x[g][st + 1]);
+              c1[g] = slice4_xor(slices, c1[g], x[g][st + 5]);
+            }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (r0 + g < K) {
+            c0[g] = slice4(slices, c0[g]);
+            c1[g] = slice4(slices, c1[g]);
+          }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (r0 + g < K) {
+            crc[r0 + g] = zmul_xor(zchunk, zmul_xor(zchunk, crc[r0 + g], c0[g]), c1[g]);
+            __asm__ volatile("" : "+v"(crc[r0 + g]));
+          }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (r0 + g < K) bitslice(x[g]);
+        encode_group_acc<K, P, MATRIX, G>(r0, x, acc);
       }
       HRS_PHASE_FENCE();
 #pragma unroll
@@ -332,7 +221,7 @@ __global__ void __launch_bounds__(THREADS) encode_crc3_kernel(const EncodeCrcArg
       uint32_t p0[P], p1[P];
       rows_piece_crcs<P>(slices, acc, p0, p1);
 #pragma unroll
-      for (int o = 0; o < P; ++o) crc[K + o] = zmul(zchunk, zmul(zchunk, crc[K + o]) ^ p0[o]) ^ p1[o];
+      for (int o = 0; o < P; ++o) crc[K + o] = zmul_xor(zchunk, zmul_xor(zchunk, crc[K + o], p0[o]), p1[o]);
     }
 #pragma unroll
     for (int r = 0; r < N; ++r) {
@@ -342,68 +231,51 @@ __global__ void __launch_bounds__(THREADS) encode_crc3_kernel(const EncodeCrcArg
   }
 }
 
-int fused_variant() {  // HRS_FUSED=1|2|3 (A/B runs); default 3
+// One 1024-thread block per CU (16 waves share the 156 KiB table image).
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedGroupDefault = 2;  // measured best (profiles/r02/fused/)
+
+int fused_variant() {  // HRS_FUSED=1: the row-serial form (A/B runs)
   static const int v = [] {
     const char* e = getenv("HRS_FUSED");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 1 && x <= 3) ? x : 3;
+    return e && e[0] == '1' ? 1 : 2;
   }();
   return v;
 }
 
-
-// One 1024-thread block per CU (16 waves share the 156 KiB table image; the
-// kernel is VALU-bound, so every wave slot counts): 3.3-3.5 ms for 1,024
-// RS(10,4) 1 MiB stripes vs 4.2-4.3 ms with 512 threads, and prefetching
-// the next row gained < 5% at the cost of VGPR spills (tools/bench_encode_crc.py).
-constexpr int kFusedThreads = 1024;
-#ifndef HRS_FUSED2_THREADS
-#define HRS_FUSED2_THREADS 512
-#endif
-constexpr int kFused2Threads = HRS_FUSED2_THREADS;
-
-int fused_ring() {
+int fused_group() {  // HRS_FUSED_GROUP: rows per lockstep group (A/B runs)
   static const int v = [] {
-    const char* e = getenv("HRS_FUSED_RING");
+    const char* e = getenv("HRS_FUSED_GROUP");
     const int x = e ? atoi(e) : 0;
-    return (x >= 1 && x <= 4) ? x : kDefaultRing;
+    return (x == 1 || x == 2 || x == 4) ? x : kFusedGroupDefault;
   }();
   return v;
 }
 
 using CrcKernel = void (*)(const EncodeCrcArgs);
 
-template <int K, int P, class MATRIX, int B>
-CrcKernel crc3_for() {
-  return encode_crc3_kernel<K, P, MATRIX, kFusedThreads, B>;
-}
-
-// The instantiated ring size closest to (not above) the requested one.
 template <int K, int P, class MATRIX>
-CrcKernel pick_crc3(int want) {
-  if (want >= 4 && K % 4 == 0) return crc3_for<K, P, MATRIX, (K % 4 == 0 ? 4 : 1)>();
-  if (want >= 3 && K % 3 == 0) return crc3_for<K, P, MATRIX, (K % 3 == 0 ? 3 : 1)>();
-  if (want >= 2 && K % 2 == 0) return crc3_for<K, P, MATRIX, (K % 2 == 0 ? 2 : 1)>();
-  return crc3_for<K, P, MATRIX, 1>();
+CrcKernel pick_kernel() {
+  if (fused_variant() == 1) return encode_crc_kernel<K, P, MATRIX, kFusedThreads>;
+  const int g = fused_group();
+  if (g == 4) return encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 4>;
+  if (g == 1) return encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 1>;
+  return encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2>;
 }
 
 template <int K, int P, class MATRIX>
 hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
   const uint64_t ntasks = a.nstripes * a.nwin;
-  const int v = fused_variant();
-  const int threads = v == 2 ? kFused2Threads : kFusedThreads;
-  const CrcKernel k = v == 1   ? encode_crc_kernel<K, P, MATRIX, kFusedThreads>
-                      : v == 2 ? encode_crc2_kernel<K, P, MATRIX, kFused2Threads>
-                               : pick_crc3<K, P, MATRIX>(fused_ring());
+  const CrcKernel k = pick_kernel<K, P, MATRIX>();
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;
-  const uint64_t per_block = threads / 64;
+  const uint64_t per_block = kFusedThreads / 64;
   uint64_t g = (ntasks + per_block - 1) / per_block;
   if (g > static_cast<uint64_t>(cus)) g = cus;
   if (g == 0) g = 1;
-  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, a);
+  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kFusedThreads), shm, s, a);
   return hipGetLastError();
 }
 
