@@ -192,6 +192,34 @@ hrs_status hrs_decode_crc(hrs_codec* codec, const uint8_t* const* read_bufs, uin
                           const int* not_to_read, int num_not_to_read, size_t len,
                           const uint32_t* crc_in, uint32_t* crc_out);
 
+/* ---- asynchronous host-buffer calls: successive rounds overlap ----
+ * An Encoder / Decoder round (Encoder.java:421-453, Decoder.java:280-372)
+ * split in two. *_submit copies the caller's rows into a free slot's pinned
+ * staging — the rows may be reused or freed as soon as it returns (the JNI
+ * shim pins Java arrays only for the call) — queues H2D -> kernel -> D2H on
+ * the slot's stream and returns a ticket; hrs_collect waits for that
+ * operation and copies its output rows out. While round r runs on the GPU the
+ * caller reads round r + 1 and submits it. A handle holds up to 4 uncollected
+ * operations (more -> HRS_EINVAL); tickets may be collected in any order.
+ * checksums = 1 adds the block CRC-32s of hrs_encode_crc / hrs_decode_crc:
+ * the running values are chained at collect time (rounds are collected in
+ * order), so they need not be known when the round is submitted. */
+hrs_status hrs_encode_submit(hrs_codec* codec, const uint8_t* const* inputs, size_t len, int checksums,
+                             uint64_t* ticket);
+hrs_status hrs_decode_submit(hrs_codec* codec, const uint8_t* const* read_bufs, const int* erased,
+                             int num_erased, const int* to_read, int num_to_read, const int* not_to_read,
+                             int num_not_to_read, size_t len, int checksums, uint64_t* ticket);
+/* outputs: p rows (encode) or num_erased rows (decode) of `len` bytes.
+ * crc_io (checksummed operations only): k + p (sources, then parities) or
+ * num_erased running java.util.zip.CRC32 values (0 = a fresh CRC32), each
+ * continued over this operation's cell (CRC32.update chaining). */
+hrs_status hrs_collect(hrs_codec* codec, uint64_t ticket, uint8_t* const* outputs, uint32_t* crc_io);
+/* Uncollected operations of this handle. */
+int hrs_pending(const hrs_codec* codec);
+/* Shape of an uncollected operation: output rows, their length, CRC values
+ * (0 if not checksummed). HRS_EINVAL for an unknown ticket. */
+hrs_status hrs_ticket_shape(const hrs_codec* codec, uint64_t ticket, int* num_outputs, size_t* len, int* num_crcs);
+
 /* ---- device-resident batches (the MI355X hot path) ----
  * Row pointers are DEVICE pointers for stripe 0; stripe s of row r lives at
  * rows[r] + s * stride. `stream` is a hipStream_t (NULL = the null stream).

@@ -155,6 +155,36 @@ class HipCode : public ErasureCode {
           h_);
   }
 
+  // Asynchronous rounds (hrs_encode_submit / hrs_decode_submit / hrs_collect):
+  // submit returns once the rows are staged; collect waits and copies out.
+  // checksums: the operation also computes the block CRC32s; collect then
+  // continues the running values in *crcs (k + p for encode, one per erased
+  // location for decode).
+  uint64_t encodeBulkSubmit(const std::vector<uint8_t*>& inputs, size_t len, bool checksums) {
+    if (static_cast<int>(inputs.size()) != stripeSize()) throw std::invalid_argument("encodeBulkSubmit: row count");
+    std::vector<const uint8_t*> in(inputs.begin(), inputs.end());
+    uint64_t t = 0;
+    check(hrs_encode_submit(h_, in.data(), len, checksums ? 1 : 0, &t), h_);
+    return t;
+  }
+
+  uint64_t decodeBulkSubmit(const std::vector<uint8_t*>& readBufs, size_t len, const std::vector<int>& erased,
+                            const std::vector<int>& toRead, const std::vector<int>& notToRead, bool checksums) {
+    if (static_cast<int>(readBufs.size()) != stripeSize() + paritySize())
+      throw std::invalid_argument("decodeBulkSubmit: row count");
+    std::vector<const uint8_t*> in(readBufs.begin(), readBufs.end());
+    uint64_t t = 0;
+    check(hrs_decode_submit(h_, in.data(), erased.data(), static_cast<int>(erased.size()), toRead.data(),
+                            static_cast<int>(toRead.size()), notToRead.data(), static_cast<int>(notToRead.size()),
+                            len, checksums ? 1 : 0, &t),
+          h_);
+    return t;
+  }
+
+  void collect(uint64_t ticket, const std::vector<uint8_t*>& outputs, std::vector<uint32_t>* crcs) {
+    check(hrs_collect(h_, ticket, outputs.data(), crcs ? crcs->data() : nullptr), h_);
+  }
+
   // RS-specific decodeBulk(readBufs, writeBufs, erasedLocation), ReedSolomonCode.java:168-185.
   void decodeBulk3(const std::vector<uint8_t*>& readBufs, const std::vector<uint8_t*>& writeBufs, size_t len,
                    const std::vector<int>& erased) {

@@ -36,6 +36,7 @@ EXPORTS = (
     "hrs_encode", "hrs_decode", "hrs_decode3", "hrs_encode_crc", "hrs_decode_crc",
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
     "hrs_encode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
+    "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
     "hrs_set_kernel_mode",
 )
 
@@ -97,6 +98,11 @@ def lib():
         "hrs_encode_crc_dev": ([P, PP, S, PP, S, S, S, P, P, P], I),
         "hrs_decode_batch_host": ([P, P, S, S, P, I, P, S, S, S, S], I),
         "hrs_encode_batch_host": ([P, P, S, S, S, S], I),
+        "hrs_encode_submit": ([P, PP, S, I, ctypes.POINTER(ctypes.c_uint64)], I),
+        "hrs_decode_submit": ([P, PP, IP, I, IP, I, IP, I, S, I, ctypes.POINTER(ctypes.c_uint64)], I),
+        "hrs_collect": ([P, ctypes.c_uint64, PP, P], I),
+        "hrs_pending": ([P], I),
+        "hrs_ticket_shape": ([P, ctypes.c_uint64, IP, ctypes.POINTER(ctypes.c_size_t), IP], I),
         "hrs_set_kernel_mode": ([P, I], I),
     }
     for name, (args, res) in sigs.items():

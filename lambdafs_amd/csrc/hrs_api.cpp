@@ -80,6 +80,22 @@ struct hrs_codec {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
   } hbatch[hrs::kHostBatchSlots];
+  // asynchronous host-buffer calls (hrs_*_submit / hrs_collect): a ring of
+  // operation slots, each pinned staging + device rows + its own stream; an
+  // operation occupies its slot from submit until it is collected
+  struct AsyncSlot {
+    uint8_t* pin = nullptr;
+    uint8_t* dev = nullptr;
+    size_t bytes = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    bool queued = false;  // GPU work was queued (len > 0)
+    uint64_t ticket = 0;
+    int nout = 0, nlive = 0, ncrc = 0;
+    size_t len = 0, pitch = 0, crc_off = 0;
+  } async[hrs::kAsyncSlots];
+  uint64_t async_tickets = 0;
   std::string err;
 };
 
@@ -830,6 +846,126 @@ hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   return st;
 }
 
+// ---------------------------------------- asynchronous host-buffer calls
+// An Encoder / Decoder round split in two: submit copies the caller's rows
+// into a free slot's pinned staging (the rows may be reused as soon as it
+// returns: Java heap arrays are pinned only for the call) and queues H2D ->
+// kernel -> D2H on the slot's stream; collect waits for that operation and
+// copies its output rows (and chained CRCs) out. While round r runs on the
+// GPU the caller reads round r + 1 and submits it, so successive rounds
+// overlap (Encoder.java:421-453 runs them back to back).
+
+hrs_status async_slot(hrs_codec* c, hrs_codec::AsyncSlot& a, size_t bytes) {
+  if (!a.stream) {
+    hipError_t e = hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(c, e, "hipStreamCreate");
+    e = hipEventCreateWithFlags(&a.done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+  }
+  if (a.bytes >= bytes) return HRS_OK;
+  (void)hipStreamSynchronize(a.stream);
+  if (a.dev) (void)hipFree(a.dev);
+  if (a.pin) (void)hipHostFree(a.pin);
+  a.dev = nullptr;
+  a.pin = nullptr;
+  a.bytes = 0;
+  hipError_t e = hipMalloc(&a.dev, bytes);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  e = hipHostMalloc(&a.pin, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  a.bytes = bytes;
+  return HRS_OK;
+}
+
+hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_t* m, int nout, int nin,
+                             const uint8_t* const* in_rows, size_t len, bool static_kp, int crc_mode) {
+  const int ncrc = crc_mode == kCrcEncode ? nin + nout : crc_mode == kCrcOutputs ? nout : 0;
+  std::vector<int> slot_of(nin, -1);
+  int nlive = 0;
+  for (int i = 0; i < nin; ++i) {
+    bool any = crc_mode == kCrcEncode;
+    for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
+    if (!any) continue;
+    if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
+    slot_of[i] = nlive++;
+  }
+  const size_t pitch = pitch_for(len);
+  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
+  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
+  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(len, 1, ncrc) : crc_off;
+  hrs_status st = async_slot(c, a, need);
+  if (st != HRS_OK) return st;
+  std::vector<hrs::CopyJob> jobs;
+  for (int i = 0; i < nin; ++i)
+    if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len});
+  hrs::CopyPool::instance().run(jobs);
+  if (nlive > 0) {
+    hipError_t e = hipMemcpyAsync(a.dev, a.pin, pitch * (nlive - 1) + len, hipMemcpyHostToDevice, a.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
+  }
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? a.dev + pitch * slot_of[i] : nullptr;
+  for (int o = 0; o < nout; ++o) dout[o] = a.dev + pitch * (nlive + o);
+  uint32_t* dcrc = reinterpret_cast<uint32_t*>(a.dev + crc_off);
+  uint32_t* draw = reinterpret_cast<uint32_t*>(a.dev + raw_off);
+  if (crc_mode == kCrcEncode)
+    st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, a.stream, draw);
+  else
+    st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, a.stream, static_kp);
+  if (st != HRS_OK) return st;
+  if (crc_mode == kCrcOutputs) {
+    std::vector<size_t> strides(nout, 0);
+    st = run_crc(c, dout.data(), strides.data(), nout, len, 1, nullptr, dcrc, a.stream, draw);
+    if (st != HRS_OK) return st;
+  }
+  const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + len;
+  hipError_t e = hipMemcpyAsync(a.pin + pitch * nlive, a.dev + pitch * nlive, back, hipMemcpyDeviceToHost, a.stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+  e = hipEventRecord(a.done, a.stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  a.nout = nout;
+  a.nlive = nlive;
+  a.ncrc = ncrc;
+  a.len = len;
+  a.pitch = pitch;
+  a.crc_off = crc_off;
+  a.queued = true;
+  return HRS_OK;
+}
+
+hrs_status async_submit(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows, size_t len,
+                        bool static_kp, int crc_mode, uint64_t* ticket) {
+  if (!ticket) return fail(c, HRS_EINVAL, "ticket is NULL");
+  *ticket = 0;
+  int free_slot = -1;
+  for (int i = 0; i < hrs::kAsyncSlots && free_slot < 0; ++i)
+    if (!c->async[i].busy) free_slot = i;
+  if (free_slot < 0)
+    return fail(c, HRS_EINVAL, "all %d asynchronous slots hold uncollected operations: collect one first",
+                hrs::kAsyncSlots);
+  hrs_codec::AsyncSlot& a = c->async[free_slot];
+  const int ncrc = crc_mode == kCrcEncode ? nin + nout : crc_mode == kCrcOutputs ? nout : 0;
+  a.queued = false;
+  a.nout = nout;
+  a.ncrc = ncrc;
+  a.len = len;
+  if (len > 0 && nout > 0) {
+    DeviceGuard g(c->device);
+    if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+    const hrs_status st = async_submit_impl(c, a, m, nout, nin, in_rows, len, static_kp, crc_mode);
+    if (st != HRS_OK) {  // leave nothing in flight in a slot marked free
+      if (a.stream) (void)hipStreamSynchronize(a.stream);
+      a.queued = false;
+      return st;
+    }
+  }
+  a.busy = true;
+  a.ticket = ++c->async_tickets;
+  *ticket = a.ticket;
+  return HRS_OK;
+}
+
 void init_encode_matrix(hrs_codec* c) {
   c->g.resize(static_cast<size_t>(c->p) * c->k);
   if (c->kind == HRS_CODE_XOR) {
@@ -1228,6 +1364,15 @@ void hrs_destroy(hrs_codec* c) {
     if (h.done) (void)hipEventDestroy(h.done);
     if (h.dev) (void)hipFree(h.dev);
     if (h.pin) (void)hipHostFree(h.pin);
+  }
+  for (auto& a : c->async) {
+    if (a.stream) {
+      (void)hipStreamSynchronize(a.stream);
+      (void)hipStreamDestroy(a.stream);
+    }
+    if (a.done) (void)hipEventDestroy(a.done);
+    if (a.dev) (void)hipFree(a.dev);
+    if (a.pin) (void)hipHostFree(a.pin);
   }
   for (auto& h : c->hbatch) {
     if (h.stream) {
@@ -1932,6 +2077,80 @@ hrs_status hrs_encode_batch_host(hrs_codec* c, uint8_t* stripes, size_t row_stri
   // parity rows 0..p-1 of each stripe are written in place
   return drain_hbatch(c, host_batch(c, stripes, row_stride, stripe_stride, c->n, stripes, row_stride, stripe_stride,
                                     p, len, nstripes, reads, compute, writes));
+}
+
+hrs_status hrs_encode_submit(hrs_codec* c, const uint8_t* const* inputs, size_t len, int checksums, uint64_t* ticket) {
+  if (!c) return HRS_EINVAL;
+  if (!inputs) return fail(c, HRS_EINVAL, "inputs is NULL");
+  return async_submit(c, c->g.data(), c->p, c->k, inputs, len, static_encode_family(c),
+                      checksums ? kCrcEncode : kCrcNone, ticket);
+}
+
+hrs_status hrs_decode_submit(hrs_codec* c, const uint8_t* const* read_bufs, const int* erased, int ne,
+                             const int* to_read, int nr, const int* ntr, int nn, size_t len, int checksums,
+                             uint64_t* ticket) {
+  if (!c) return HRS_EINVAL;
+  if (!read_bufs || ne < 0 || nn < 0 || nr < 0 || (ne > 0 && !erased) || (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) ||
+      (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+    return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  if (ne > 0) {
+    hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d, to_read, to_read ? nr : -1);
+    if (st != HRS_OK) return st;
+  }
+  return async_submit(c, d, ne, c->n, read_bufs, ne > 0 ? len : 0, false, checksums ? kCrcOutputs : kCrcNone, ticket);
+}
+
+hrs_status hrs_collect(hrs_codec* c, uint64_t ticket, uint8_t* const* outputs, uint32_t* crc_io) {
+  if (!c) return HRS_EINVAL;
+  hrs_codec::AsyncSlot* a = nullptr;
+  for (auto& s : c->async)
+    if (s.busy && s.ticket == ticket) a = &s;
+  if (!a) return fail(c, HRS_EINVAL, "no uncollected operation with ticket %llu", static_cast<unsigned long long>(ticket));
+  if (a->nout > 0 && a->len > 0 && !outputs) return fail(c, HRS_EINVAL, "outputs is NULL");
+  if (a->ncrc > 0 && !crc_io) return fail(c, HRS_EINVAL, "crc_io is NULL for a checksummed operation");
+  for (int o = 0; o < a->nout && a->len > 0; ++o)
+    if (!outputs[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  hrs_status st = HRS_OK;
+  if (a->queued) {
+    hipError_t e = hipEventSynchronize(a->done);
+    if (e != hipSuccess) st = hip_fail(c, e, "hipEventSynchronize");
+  }
+  if (st == HRS_OK && a->queued) {
+    std::vector<hrs::CopyJob> jobs;
+    for (int o = 0; o < a->nout; ++o) jobs.push_back({outputs[o], a->pin + a->pitch * (a->nlive + o), a->len});
+    hrs::CopyPool::instance().run(jobs);
+  }
+  if (st == HRS_OK && a->ncrc > 0 && a->queued) {  // CRC32.update chaining: crc = Z_len(crc) ^ crc(cell)
+    const uint32_t* part = reinterpret_cast<const uint32_t*>(a->pin + a->crc_off);
+    const hrs::crc::Mat& z = crc_zmat(c, a->len);
+    for (int r = 0; r < a->ncrc; ++r) crc_io[r] = hrs::crc::apply(z, crc_io[r]) ^ part[r];
+  }
+  a->busy = false;
+  a->queued = false;
+  return st;
+}
+
+hrs_status hrs_ticket_shape(const hrs_codec* c, uint64_t ticket, int* num_outputs, size_t* len, int* num_crcs) {
+  if (!c) return HRS_EINVAL;
+  for (const auto& s : c->async)
+    if (s.busy && s.ticket == ticket) {
+      if (num_outputs) *num_outputs = s.nout;
+      if (len) *len = s.len;
+      if (num_crcs) *num_crcs = s.ncrc;
+      return HRS_OK;
+    }
+  return HRS_EINVAL;
+}
+
+int hrs_pending(const hrs_codec* c) {
+  if (!c) return -1;
+  int n = 0;
+  for (const auto& s : c->async) n += s.busy;
+  return n;
 }
 
 hrs_status hrs_apply_dev(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,

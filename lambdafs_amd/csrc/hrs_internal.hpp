@@ -62,6 +62,7 @@ int device_cu_count();  // CUs of the current device (cached)
 
 constexpr int kBatchMaxIn = 16;
 constexpr int kHostBatchSlots = 3;  // chunk slots of the host-memory batch pipeline
+constexpr int kAsyncSlots = 4;      // operations in flight per handle (hrs_*_submit / hrs_collect)
 struct BatchPlan {            // one erasure pattern, a device table entry
   int nin;                    // live survivor rows read
   int nout;                   // erased rows written

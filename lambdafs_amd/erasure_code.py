@@ -368,6 +368,69 @@ class _HipErasureCode(ErasureCode):
             crc_out.ctypes.data))
         return [int(x) for x in crc_out]
 
+    # -- asynchronous rounds (hrs_*_submit / hrs_collect): round r computes on
+    #    the GPU while the caller reads round r + 1; host rows only
+    def encodeBulkAsync(self, inputs, checksums=False):
+        """Submit an encodeBulk (plus the Encoder's block checksums when
+        `checksums`); returns a ticket for collect(). The input rows may be
+        reused as soon as this returns."""
+        if len(inputs) != self._k:
+            raise ValueError(f"encodeBulk needs {self._k} inputs")
+        ins = _Rows(inputs, writable=False)
+        if self._placement(ins) is not None:
+            raise ValueError("asynchronous calls take host rows")
+        t = ctypes.c_uint64(0)
+        self._check(_lib.lib().hrs_encode_submit(self._handle(), ins.ptrs, ins.len, int(bool(checksums)),
+                                                 ctypes.byref(t)))
+        if self.zero_inputs_after_encode:
+            for v in ins.views:
+                if v.flags["WRITEABLE"]:
+                    v[:] = 0
+        return t.value
+
+    def decodeBulkAsync(self, readBufs, erasedLocations, locationsToRead, locationsNotToRead, checksums=False):
+        """Submit a 5-arg decodeBulk (plus the repaired blocks' CRC32s when
+        `checksums`); returns a ticket for collect()."""
+        n = self._k + self._p
+        if len(readBufs) != n:
+            raise ValueError(f"decodeBulk needs {n} read buffers")
+        ntr = set(locationsNotToRead)
+        reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
+                      writable=False, allow_none=True)
+        if self._placement(reads) is not None:
+            raise ValueError("asynchronous calls take host rows")
+        locationsToRead = locationsToRead or []
+        t = ctypes.c_uint64(0)
+        self._check(_lib.lib().hrs_decode_submit(
+            self._handle(), reads.ptrs, int_array(erasedLocations), len(erasedLocations), int_array(locationsToRead),
+            len(locationsToRead), int_array(locationsNotToRead), len(locationsNotToRead), reads.len,
+            int(bool(checksums)), ctypes.byref(t)))
+        return t.value
+
+    def collect(self, ticket, outputs, crcs=None):
+        """Wait for a submitted operation and copy its output rows into
+        `outputs` (p rows for encode, one per erased location for decode).
+        A checksummed operation returns its CRC32 values continued from
+        `crcs` (the running values; None = fresh CRC32 objects), else None."""
+        nout, ln, ncrc = ctypes.c_int(0), ctypes.c_size_t(0), ctypes.c_int(0)
+        self._check(_lib.lib().hrs_ticket_shape(self._handle(), int(ticket), ctypes.byref(nout), ctypes.byref(ln),
+                                                ctypes.byref(ncrc)))
+        if len(outputs) != nout.value:
+            raise ValueError(f"this operation has {nout.value} output rows")
+        outs = _Rows(outputs, writable=True)
+        if outputs and outs.len < ln.value:
+            raise ValueError("output rows shorter than the operation's rows")
+        crc = np.zeros(max(1, ncrc.value), dtype=np.uint32)
+        if ncrc.value and crcs is not None:
+            crc[: ncrc.value] = np.asarray(crcs, dtype=np.uint64).astype(np.uint32)
+        self._check(_lib.lib().hrs_collect(self._handle(), int(ticket), outs.ptrs,
+                                           crc.ctypes.data if ncrc.value else None))
+        return [int(x) for x in crc[: ncrc.value]] if ncrc.value else None
+
+    def pending(self):
+        """Submitted operations not yet collected (at most 4 per codec)."""
+        return int(_lib.lib().hrs_pending(self._handle()))
+
     def _apply_dev(self, m, reads, writes):
         stream = _lib.torch.cuda.current_stream(reads.device).cuda_stream
         m = np.ascontiguousarray(m, dtype=np.uint8)

@@ -81,6 +81,47 @@ public class HipReedSolomonCode extends ErasureCode {
         locationsNotToRead, readBufs[0].length, crcs);
   }
 
+  /**
+   * Asynchronous rounds for a caller that keeps the GPU busy across rounds
+   * (Encoder.java:421-453 runs encodeBulk rounds back to back): the round is
+   * staged and queued, and the caller may reuse `inputs` at once (they are
+   * zeroed, as encodeBulk does); collect(ticket, writeBufs) later waits for it.
+   * Up to 4 rounds may be outstanding per codec.
+   */
+  public long encodeBulkAsync(byte[][] inputs) throws IOException {
+    long t = HrsNative.encodeSubmit(nativeCodec, inputs, inputs[0].length, false);
+    for (byte[] in : inputs) {
+      Arrays.fill(in, (byte) 0);
+    }
+    return t;
+  }
+
+  /** encodeBulkAsync plus the block checksums, continued by collect(ticket, outputs, crcs). */
+  public long encodeBulkAsyncWithChecksums(byte[][] inputs) throws IOException {
+    long t = HrsNative.encodeSubmit(nativeCodec, inputs, inputs[0].length, true);
+    for (byte[] in : inputs) {
+      Arrays.fill(in, (byte) 0);
+    }
+    return t;
+  }
+
+  /** The 5-arg decodeBulk round, submitted (Decoder.java:352-353). */
+  public long decodeBulkAsync(byte[][] readBufs, int[] erasedLocations, int[] locationsToRead,
+      int[] locationsNotToRead, boolean checksums) throws IOException {
+    return HrsNative.decodeSubmit(nativeCodec, readBufs, erasedLocations, locationsToRead, locationsNotToRead,
+        readBufs[0].length, checksums);
+  }
+
+  /** Waits for a submitted round and copies its output rows into `outputs`. */
+  public void collect(long ticket, byte[][] outputs) throws IOException {
+    HrsNative.collect(nativeCodec, ticket, outputs, null);
+  }
+
+  /** collect for a checksummed round: crcs (k + p or one per erased location) continued in place. */
+  public void collect(long ticket, byte[][] outputs, int[] crcs) throws IOException {
+    HrsNative.collect(nativeCodec, ticket, outputs, crcs);
+  }
+
   /** Same result as ReedSolomonCode.decodeBulk 5-arg (ReedSolomonCode.java:191-211). */
   @Override
   public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocations,

@@ -44,4 +44,16 @@ final class HrsNative {
   // hrs_decode_crc: crcs[erased.length] continued in place over writeBufs
   static native void decodeCrc(long codec, byte[][] readBufs, byte[][] writeBufs, int[] erased, int[] toRead,
       int[] notToRead, int len, int[] crcs) throws IOException;
+
+  // asynchronous rounds: hrs_encode_submit / hrs_decode_submit return a ticket
+  // once the rows are staged; collect waits and copies the outputs (and, for
+  // a checksummed round, continues crcs in place)
+  static native long encodeSubmit(long codec, byte[][] inputs, int len, boolean checksums) throws IOException;
+
+  static native long decodeSubmit(long codec, byte[][] readBufs, int[] erased, int[] toRead, int[] notToRead,
+      int len, boolean checksums) throws IOException;
+
+  static native void collect(long codec, long ticket, byte[][] outputs, int[] crcs) throws IOException;
+
+  static native int pending(long codec);
 }

@@ -412,3 +412,128 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_decodeCrc(JNIEnv* 
   }
   decode_common(env, h, readBufs, writeBufs, erased, toRead, notToRead, len, crcs, 0);
 }
+
+/* ------------------------------------------------- asynchronous rounds */
+
+/* hrs_encode_submit: stages the rows (pinned only for this call), queues the
+ * round, returns the ticket. checksums != 0 adds the block CRC32s (chained by
+ * collect). */
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_encodeSubmit(JNIEnv* env, jclass cls, jlong h,
+                                                                           jobjectArray inputs, jint len,
+                                                                           jboolean checksums) {
+  (void)cls;
+  hrs_codec* c = handle(env, h);
+  if (!c || check_len(env, len) || open_frame(env)) return 0;
+  Rows in;
+  in.n = 0;
+  uint64_t ticket = 0;
+  if (fetch_rows(env, inputs, "inputs", hrs_stripe_size(c), 1, NULL, len, &in) == 0) {
+    int ok = pin_rows(env, &in) == 0;
+    hrs_status st = ok ? hrs_encode_submit(c, (const uint8_t* const*)in.ptr, (size_t)len, checksums ? 1 : 0, &ticket)
+                       : HRS_OK;
+    unpin_rows(env, &in, JNI_ABORT);
+    if (ok && st != HRS_OK) throw_status(env, st, c);
+  }
+  close_frame(env);
+  return (jlong)ticket;
+}
+
+/* hrs_decode_submit (the 5-arg decodeBulk round). */
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_decodeSubmit(JNIEnv* env, jclass cls, jlong h,
+                                                                           jobjectArray readBufs, jintArray erased,
+                                                                           jintArray toRead, jintArray notToRead,
+                                                                           jint len, jboolean checksums) {
+  (void)cls;
+  hrs_codec* c = handle(env, h);
+  if (!c || check_len(env, len)) return 0;
+  struct dec_arg* a = (struct dec_arg*)calloc(1, sizeof *a);
+  Rows* in = (Rows*)malloc(sizeof(Rows));
+  uint64_t ticket = 0;
+  if (!a || !in) {
+    free(a);
+    free(in);
+    throw_msg(env, "java/lang/OutOfMemoryError", "decode arguments");
+    return 0;
+  }
+  if (open_frame(env)) {
+    free(a);
+    free(in);
+    return 0;
+  }
+  in->n = 0;
+  unsigned char may_be_null[MAX_ROWS];
+  a->ne = copy_ints(env, erased, "erasedLocations", 0, a->e);
+  if (a->ne < 0) goto done;
+  a->has_to_read = toRead != NULL;
+  a->nr = copy_ints(env, toRead, "locationsToRead", 1, a->r);
+  if (a->nr < 0) goto done;
+  a->nn = copy_ints(env, notToRead, "locationsNotToRead", 0, a->ntr);
+  if (a->nn < 0) goto done;
+  memset(may_be_null, 0, sizeof may_be_null);
+  for (int j = 0; j < a->nn; j++)
+    if (a->ntr[j] >= 0 && a->ntr[j] < MAX_ROWS) may_be_null[a->ntr[j]] = 1;
+  if (fetch_rows(env, readBufs, "readBufs", hrs_stripe_size(c) + hrs_parity_size(c), 1, may_be_null, len, in))
+    goto done;
+  {
+    int ok = pin_rows(env, in) == 0;
+    hrs_status st = ok ? hrs_decode_submit(c, (const uint8_t* const*)in->ptr, a->e, a->ne,
+                                           a->has_to_read ? a->r : NULL, a->nr, a->ntr, a->nn, (size_t)len,
+                                           checksums ? 1 : 0, &ticket)
+                       : HRS_OK;
+    unpin_rows(env, in, JNI_ABORT);
+    if (ok && st != HRS_OK) throw_status(env, st, c);
+  }
+done:
+  close_frame(env);
+  free(in);
+  free(a);
+  return (jlong)ticket;
+}
+
+/* hrs_collect: waits for the round, copies its output rows into `outputs`
+ * (p rows / one per erased location, each at least the round's length); a
+ * checksummed round continues the running CRC32s in `crcs` (k + p / one per
+ * erased location) in place. */
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_collect(JNIEnv* env, jclass cls, jlong h, jlong ticket,
+                                                                     jobjectArray outputs, jintArray crcs) {
+  (void)cls;
+  hrs_codec* c = handle(env, h);
+  if (!c) return;
+  int nout = 0, ncrc = 0;
+  size_t len = 0;
+  if (hrs_ticket_shape(c, (uint64_t)ticket, &nout, &len, &ncrc) != HRS_OK) {
+    throw_msg(env, kIAE, "no uncollected operation with ticket %lld", (long long)ticket);
+    return;
+  }
+  if (open_frame(env)) return;
+  uint32_t crc[MAX_ROWS];
+  Rows out;
+  out.n = 0;
+  if (ncrc > 0) {
+    const int got = copy_ints(env, crcs, "crcs", 0, (int*)crc);
+    if (got < 0) goto done;
+    if (got != ncrc) {
+      throw_msg(env, kIAE, "crcs has %d entries, the operation keeps %d", got, ncrc);
+      goto done;
+    }
+  }
+  if (fetch_rows(env, outputs, "outputs", nout, 0, NULL, (jint)len, &out)) goto done;
+  {
+    int ok = pin_rows(env, &out) == 0;
+    hrs_status st = ok ? hrs_collect(c, (uint64_t)ticket, out.ptr, ncrc > 0 ? crc : NULL) : HRS_OK;
+    unpin_rows(env, &out, 0);
+    if (ok && st != HRS_OK) {
+      throw_status(env, st, c);
+      goto done;
+    }
+    if (ok && ncrc > 0) (*env)->SetIntArrayRegion(env, crcs, 0, ncrc, (const jint*)crc);
+  }
+done:
+  close_frame(env);
+}
+
+JNIEXPORT jint JNICALL Java_io_hops_erasure_1coding_HrsNative_pending(JNIEnv* env, jclass cls, jlong h) {
+  (void)cls;
+  hrs_codec* c = handle(env, h);
+  return c ? hrs_pending(c) : 0;
+}

@@ -33,6 +33,9 @@
 // decodeBulk of bufSize cells of RS(k,p); a checked pass (every round vs the
 // oracle's parity / the original cells) then a timed pass; prints the
 // aggregate user-data GiB/s (k * bufSize per call).
+// --async=D : Encoder / Decoder rounds pipelined D deep through
+// encodeBulkSubmit / decodeBulkSubmit / collect vs the synchronous calls
+// (see async_mode).
 // Prints one JSON line; exit status 0 iff everything matched.
 #include <zlib.h>
 
@@ -272,9 +275,125 @@ int threads_mode(int k, int p, size_t buf, int nthreads, int rounds, uint64_t se
   return ok ? 0 : 1;
 }
 
+// --async=D : one Encoder.encodeStripe and one Decoder.fixErasedBlockImpl of a
+// `block`-byte stripe in bufSize rounds, synchronous (encodeBulkCrc /
+// decodeBulkCrc per round) and pipelined D rounds deep (submit round r, read
+// round r + 1 while it runs, collect round r - D + 1). Both produce every
+// parity / repaired cell and the chained block CRC32s; both are checked
+// against the oracle and zlib; prints the user-data GiB/s of each.
+int async_mode(int k, int p, size_t block, size_t buf, int nerased, int depth, uint64_t seed) {
+  const int n = k + p;
+  hrs::HipReedSolomonCode code(k, p, 0);
+  std::vector<std::vector<uint8_t>> stripe(n, std::vector<uint8_t>(block));
+  for (int i = 0; i < k; ++i) fill(stripe[p + i], seed * 1000 + i);
+  {
+    std::vector<std::vector<uint8_t>> cp(stripe.begin() + p, stripe.end());
+    std::vector<uint8_t*> ip(k), op(p);
+    for (int i = 0; i < k; ++i) ip[i] = cp[i].data();
+    for (int r = 0; r < p; ++r) op[r] = stripe[r].data();
+    orc_rs_encode_bulk(k, p, ip.data(), op.data(), block);
+  }
+  std::vector<uint32_t> stored(n);
+  for (int l = 0; l < n; ++l) stored[l] = crc(0, stripe[l].data(), block);
+  uint64_t z = seed;
+  std::vector<int> erased;
+  while (static_cast<int>(erased.size()) < nerased) {
+    const int loc = static_cast<int>(splitmix(z) % n);
+    if (!contains(erased, loc)) erased.push_back(loc);
+  }
+  std::vector<int> ea, ta, na;
+  decoder_arrays(n, erased, code.locationsToReadForDecode(erased), ea, ta, na);
+  const int ne = static_cast<int>(ea.size());
+  const size_t nrounds = (block + buf - 1) / buf;
+  // read buffers (ParallelStreamReader): the Encoder's k, the Decoder's reads
+  std::vector<std::vector<uint8_t>> rbuf(n, std::vector<uint8_t>(buf));
+  std::vector<std::vector<uint8_t>> wbuf(std::max(p, ne), std::vector<uint8_t>(buf));
+  std::vector<uint8_t*> enc_in(k), dec_in(n, nullptr), wp;
+  for (int i = 0; i < k; ++i) enc_in[i] = rbuf[p + i].data();
+  for (int l : ta) dec_in[l] = rbuf[l].data();
+  std::vector<std::vector<uint8_t>> parity_out(p, std::vector<uint8_t>(block)), fixed(ne, std::vector<uint8_t>(block));
+  size_t bad_at[2][2] = {{0, 0}, {0, 0}};  // [sync|async][encode|decode]
+  double secs[2][2] = {{0, 0}, {0, 0}};
+  for (int rep = 0; rep < 2; ++rep)       // 0: warm-up, 1: timed (both checked)
+    for (int mode = 0; mode < 2; ++mode) {
+      // ------------------------------------------------------------ Encoder
+      std::vector<uint32_t> ecrc(n, 0);
+      std::vector<uint64_t> tk(nrounds);
+      auto t0 = std::chrono::steady_clock::now();
+      auto encode_out = [&](size_t r) {
+        std::vector<uint8_t*> op(p);
+        for (int o = 0; o < p; ++o) op[o] = parity_out[o].data() + r * buf;
+        return op;
+      };
+      for (size_t r = 0; r < nrounds + (mode ? depth - 1 : 0); ++r) {
+        if (r < nrounds) {
+          const size_t off = r * buf, len = std::min(buf, block - off);
+          for (int i = 0; i < k; ++i) std::memcpy(rbuf[p + i].data(), stripe[p + i].data() + off, len);
+          if (mode == 0) {
+            std::vector<uint32_t> c(ecrc);
+            std::vector<uint8_t*> wb(p);
+            for (int o = 0; o < p; ++o) wb[o] = wbuf[o].data();
+            code.encodeBulkCrc(enc_in, wb, len, c);
+            ecrc = c;
+            for (int o = 0; o < p; ++o) std::memcpy(parity_out[o].data() + off, wbuf[o].data(), len);  // out.write
+            continue;
+          }
+          tk[r] = code.encodeBulkSubmit(enc_in, len, true);
+        }
+        if (mode == 1 && r + 1 >= static_cast<size_t>(depth)) {
+          const size_t q = r + 1 - depth;
+          code.collect(tk[q], encode_out(q), &ecrc);  // collect writes straight into the output block
+        }
+      }
+      secs[mode][0] += rep ? std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() : 0;
+      for (int o = 0; o < p; ++o) bad_at[mode][0] += parity_out[o] != stripe[o];
+      for (int i = 0; i < n; ++i)  // ecrc: sources then parities; stored: by location (parity first)
+        bad_at[mode][0] += ecrc[i] != stored[i < k ? p + i : i - k];
+      for (auto& v : parity_out) std::fill(v.begin(), v.end(), 0);
+      // ------------------------------------------------------------ Decoder
+      std::vector<uint32_t> dcrc(ne, 0);
+      t0 = std::chrono::steady_clock::now();
+      for (size_t r = 0; r < nrounds + (mode ? depth - 1 : 0); ++r) {
+        if (r < nrounds) {
+          const size_t off = r * buf, len = std::min(buf, block - off);
+          for (int l : ta) std::memcpy(rbuf[l].data(), stripe[l].data() + off, len);
+          if (mode == 0) {
+            // not-to-read rows: NULL (zeros, StripeReader.java:106-124); a
+            // non-NULL row would be read as the Java decode reads it
+            wp.assign(ne, nullptr);
+            for (int j = 0; j < ne; ++j) wp[j] = wbuf[j].data();
+            code.decodeBulkCrc(dec_in, wp, len, ea, ta, na, dcrc);
+            for (int j = 0; j < ne; ++j) std::memcpy(fixed[j].data() + off, wbuf[j].data(), len);
+            continue;
+          }
+          tk[r] = code.decodeBulkSubmit(dec_in, len, ea, ta, na, true);
+        }
+        if (mode == 1 && r + 1 >= static_cast<size_t>(depth)) {
+          const size_t q = r + 1 - depth;
+          std::vector<uint8_t*> op(ne);
+          for (int j = 0; j < ne; ++j) op[j] = fixed[j].data() + q * buf;
+          code.collect(tk[q], op, &dcrc);
+        }
+      }
+      secs[mode][1] += rep ? std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() : 0;
+      for (int j = 0; j < ne; ++j) bad_at[mode][1] += fixed[j] != stripe[ea[j]] || dcrc[j] != stored[ea[j]];
+      for (auto& v : fixed) std::fill(v.begin(), v.end(), 0);
+    }
+  const double user = static_cast<double>(k) * block / (1u << 30);
+  const size_t bad = bad_at[0][0] + bad_at[0][1] + bad_at[1][0] + bad_at[1][1];
+  const bool ok = bad == 0;
+  printf("{\"mode\": \"async\", \"k\": %d, \"p\": %d, \"block\": %zu, \"buf\": %zu, \"depth\": %d, "
+         "\"erased\": %d, \"mismatches\": %zu, \"bad_sync_enc_dec\": [%zu, %zu], \"bad_async_enc_dec\": [%zu, %zu], "
+         "\"encode_sync_GiBps\": %.3f, \"encode_async_GiBps\": %.3f, "
+         "\"decode_sync_GiBps\": %.3f, \"decode_async_GiBps\": %.3f, \"ok\": %s}\n",
+         k, p, block, buf, depth, ne, bad, bad_at[0][0], bad_at[0][1], bad_at[1][0], bad_at[1][1], user / secs[0][0], user / secs[1][0], user / secs[0][1],
+         user / secs[1][1], ok ? "true" : "false");
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   bool host_only = false, use_xor = false, use_nrs = false, use_src = false;
-  int src_s = 0, grow = -1, threads = 0, rounds = 16;
+  int src_s = 0, grow = -1, threads = 0, rounds = 16, depth = 0;
   std::vector<std::string> pos;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -288,6 +407,8 @@ int main(int argc, char** argv) {
       grow = atoi(a.c_str() + 7);
     else if (a.rfind("--threads=", 0) == 0)
       threads = atoi(a.c_str() + 10);
+    else if (a.rfind("--async=", 0) == 0)
+      depth = atoi(a.c_str() + 8);
     else if (a.rfind("--rounds=", 0) == 0)
       rounds = atoi(a.c_str() + 9);
     else if (a.rfind("--src=", 0) == 0) {
@@ -307,6 +428,7 @@ int main(int argc, char** argv) {
   try {
     if (grow >= 0) return grow_mode(k, p, block, buf, grow, seed);
     if (threads > 0) return threads_mode(k, p, buf, threads, rounds, seed);
+    if (depth > 0) return async_mode(k, p, block, buf, nerased, depth, seed);
   } catch (const std::exception& e) {
     printf("{\"error\": \"%s\", \"ok\": false}\n", e.what());
     return 2;

@@ -131,6 +131,27 @@ void rs_checks(int k, int p) {
   for (auto& r : rows) r = buf.data();
   for (auto& o : outs) o = buf.data();
   expect(hrs_encode(c, rows.data(), outs.data(), 64) == HRS_EDEVICE, "host-only encode -> EDEVICE");
+  // asynchronous rounds: no slot is taken by a failed submit
+  uint64_t t = 7;
+  expect(hrs_encode_submit(c, rows.data(), 64, 1, &t) == HRS_EDEVICE && t == 0, "host-only submit -> EDEVICE");
+  expect(hrs_encode_submit(c, rows.data(), 64, 0, nullptr) == HRS_EINVAL, "submit without a ticket");
+  expect(hrs_pending(c) == 0, "failed submits hold no slot");
+  // zero-length rounds need no device: a ticket that collects to nothing
+  uint64_t z[5] = {0, 0, 0, 0, 0};
+  int taken = 0;
+  for (auto& zt : z) taken += hrs_encode_submit(c, rows.data(), 0, 1, &zt) == HRS_OK;
+  expect(taken == 4 && hrs_pending(c) == 4 && z[4] == 0, "4 slots, the 5th submit refused");
+  int nout = -1, ncrc = -1;
+  size_t ln = 1;
+  expect(hrs_ticket_shape(c, z[2], &nout, &ln, &ncrc) == HRS_OK && nout == p && ln == 0 && ncrc == n,
+         "ticket shape");
+  std::vector<uint32_t> crc(n, 0x1234u);
+  expect(hrs_collect(c, z[2], outs.data(), nullptr) == HRS_EINVAL, "checksummed collect needs crc_io");
+  expect(hrs_collect(c, z[2], outs.data(), crc.data()) == HRS_OK && crc[0] == 0x1234u && hrs_pending(c) == 3,
+         "empty round leaves the running CRCs");
+  expect(hrs_collect(c, z[2], outs.data(), crc.data()) == HRS_EINVAL, "a ticket collects once");
+  for (int i : {0, 1, 3}) expect(hrs_collect(c, z[i], outs.data(), crc.data()) == HRS_OK, "collect the rest");
+  expect(hrs_pending(c) == 0 && hrs_ticket_shape(c, z[0], nullptr, nullptr, nullptr) == HRS_EINVAL, "all collected");
   hrs_destroy(c);
 }
 

@@ -21,7 +21,9 @@
  *          host-only handle (no GPU needed).
  *  --gpu : HrsNative.encode / decode / decode3 / encodeCrc / decodeCrc of
  *          RS(10,4) with 1 MiB cells vs the oracle (and zlib for the CRCs),
- *          bit-exact; short rows on a live handle; xor / nrs / src encodes.
+ *          bit-exact; short rows on a live handle; asynchronous rounds
+ *          (encodeSubmit / decodeSubmit / collect: 2 deep with chained CRCs,
+ *          the 4-slot limit, out-of-order collects); xor / nrs / src encodes.
  * Prints one JSON line; exit status 0 iff every check passed.
  */
 #define _GNU_SOURCE
@@ -362,6 +364,15 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_decodeCrc(JNIEnv*,
                                                                        jobjectArray, jintArray, jintArray, jintArray,
                                                                        jint, jintArray);
 
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_encodeSubmit(JNIEnv*, jclass, jlong, jobjectArray, jint,
+                                                                           jboolean);
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_decodeSubmit(JNIEnv*, jclass, jlong, jobjectArray,
+                                                                           jintArray, jintArray, jintArray, jint,
+                                                                           jboolean);
+JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_collect(JNIEnv*, jclass, jlong, jlong, jobjectArray,
+                                                                     jintArray);
+JNIEXPORT jint JNICALL Java_io_hops_erasure_1coding_HrsNative_pending(JNIEnv*, jclass, jlong);
+
 #define NS(f) Java_io_hops_erasure_1coding_HrsNative_##f
 
 /* ---------------------------------------------------------------- checks */
@@ -527,6 +538,25 @@ static int cpu_checks(void) {
                 NS(decodeCrc)(env, NULL, h, rows(n, L, 2), rows(1, L, 0), E, TR, NTR, L, new_ints(2, NULL)));
   EXPECT_THROWN("decodeCrc ok shapes", kIOE,
                 NS(decodeCrc)(env, NULL, h, rows(n, L, 2), rows(1, L, 0), E, TR, NTR, L, new_ints(1, NULL)));
+
+  /* asynchronous rounds */
+  EXPECT_THROWN("encodeSubmit host-only handle", kIOE, NS(encodeSubmit)(env, NULL, h, rows(k, L, 1), L, JNI_TRUE));
+  EXPECT_THROWN("encodeSubmit 9 inputs", kIAE, NS(encodeSubmit)(env, NULL, h, rows(k - 1, L, 1), L, JNI_FALSE));
+  {
+    jobjectArray in = rows(k, L, 1);
+    set_obj(in, 5, new_bytes(L - 2));
+    EXPECT_THROWN("encodeSubmit short row", kAIOOBE, NS(encodeSubmit)(env, NULL, h, in, L, JNI_FALSE));
+  }
+  EXPECT_THROWN("decodeSubmit host-only handle", kIOE,
+                NS(decodeSubmit)(env, NULL, h, rows(n, L, 2), E, TR, NTR, L, JNI_FALSE));
+  EXPECT_THROWN("decodeSubmit erased null", kNPE,
+                NS(decodeSubmit)(env, NULL, h, rows(n, L, 2), NULL, TR, NTR, L, JNI_FALSE));
+  EXPECT_THROWN("collect unknown ticket", kIAE, NS(collect)(env, NULL, h, 12345, rows(p, L, 0), NULL));
+  {
+    jint pend = -1;
+    CALL("pending", pend = NS(pending)(env, NULL, h));
+    expect(pend == 0 && !vm.pending, "pending on an idle handle");
+  }
   hrs_destroy(c);
   return 0;
 }
@@ -665,6 +695,66 @@ static int gpu_checks(void) {
     int same = !vm.pending;
     for (int r = 0; r < p; r++) same &= memcmp(bytes_of(row(lo, r)), ref_out[r], 4096 + 3) == 0;
     expect(same, "encode of a row prefix");
+  }
+  /* asynchronous Encoder rounds, depth 2: submit round r, collect round r - 1
+   * (parity vs the oracle, CRC32s chained across rounds vs zlib) */
+  {
+    const int R = 4;
+    const jsize Lr = 1 << 20;
+    jobjectArray rin[4];
+    jlong tk[4];
+    uint32_t want[14];
+    memset(want, 0, sizeof want);
+    jintArray run = new_ints(14, NULL);
+    int ok = 1;
+    for (int r = 0; r <= R; ++r) {
+      if (r < R) {
+        rin[r] = rows(k, Lr, 40 + (uint64_t)r);
+        for (int i = 0; i < k; i++) want[i] = zcrc(want[i], bytes_of(row(rin[r], i)), (size_t)Lr);
+        CALL("encodeSubmit", tk[r] = NS(encodeSubmit)(env, NULL, h, rin[r], Lr, JNI_TRUE));
+        ok &= !vm.pending && tk[r] != 0;
+      }
+      if (r >= 1) {
+        const int q = r - 1;
+        jobjectArray out = rows(p, Lr, 0);
+        CALL("collect", NS(collect)(env, NULL, h, tk[q], out, run));
+        ok &= !vm.pending;
+        uint8_t* ri[10];
+        uint8_t* ro[4];
+        for (int i = 0; i < k; i++) {
+          ri[i] = malloc((size_t)Lr);
+          memcpy(ri[i], bytes_of(row(rin[q], i)), (size_t)Lr);
+        }
+        for (int o = 0; o < p; o++) ro[o] = calloc(1, (size_t)Lr);
+        orc_rs_encode_bulk(k, p, ri, ro, (size_t)Lr);
+        for (int o = 0; o < p; o++) {
+          ok &= memcmp(bytes_of(row(out, o)), ro[o], (size_t)Lr) == 0;
+          want[k + o] = zcrc(want[k + o], ro[o], (size_t)Lr);
+          free(ro[o]);
+        }
+        for (int i = 0; i < k; i++) free(ri[i]);
+      }
+    }
+    for (int i = 0; i < 14; i++) ok &= (uint32_t)ints_of(run)[i] == want[i];
+    jint pend = -1;
+    CALL("pending", pend = NS(pending)(env, NULL, h));
+    expect(ok && pend == 0, "async encode rounds (depth 2, chained CRCs) vs the oracle and zlib");
+    /* an asynchronous decode round (the 5-arg decodeBulk of a codeword) */
+    jlong td = 0;
+    CALL("decodeSubmit",
+         td = NS(decodeSubmit)(env, NULL, h, cw, new_ints(1, er1), new_ints(10, tr1), new_ints(4, ntr1), L, JNI_TRUE));
+    jobjectArray dw = rows(1, L, 0);
+    jintArray dc = new_ints(1, NULL);
+    CALL("collect decode", NS(collect)(env, NULL, h, td, dw, dc));
+    expect(!vm.pending && memcmp(bytes_of(row(dw, 0)), bytes_of(row(in, 0)), (size_t)L) == 0 &&
+               (uint32_t)ints_of(dc)[0] == zcrc(0, bytes_of(row(in, 0)), (size_t)L),
+           "async decode round + repaired CRC");
+    /* the slot limit: 4 outstanding rounds, the 5th is refused */
+    jlong t5[5];
+    for (int r = 0; r < 4; ++r) CALL("encodeSubmit x4", t5[r] = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
+    EXPECT_THROWN("fifth outstanding round", kIAE, t5[4] = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
+    for (int r = 3; r >= 0; --r) CALL("collect out of order", NS(collect)(env, NULL, h, t5[r], rows(p, 4096, 0), NULL));
+    expect(!vm.pending, "collect in any order");
   }
   CALL("destroy", NS(destroy)(env, NULL, h));
 

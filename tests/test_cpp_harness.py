@@ -105,3 +105,16 @@ def test_harness_concurrent_handles(cuda, threads):
     and the original cells."""
     rc, res = run(f"--threads={threads}", "--rounds=12", 10, 4, 1 << 20, 1 << 20, 1, 31)
     assert rc == 0 and res["ok"], res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth,nerased", [(2, 2), (4, 4)])
+def test_harness_async_rounds_vs_sync(cuda, depth, nerased):
+    """Encoder.encodeStripe / Decoder.fixErasedBlockImpl of an RS(10,4)
+    stripe (16 MiB blocks + a ragged tail, 1 MiB rounds) pipelined `depth`
+    rounds deep through encodeBulkSubmit / decodeBulkSubmit / collect and
+    synchronously: every parity / repaired cell vs the oracle and the chained
+    block CRC32s vs zlib, in both modes."""
+    rc, res = run(f"--async={depth}", 10, 4, (16 << 20) + 4097, 1 << 20, nerased, 17)
+    assert rc == 0 and res["ok"], res
+    assert res["mismatches"] == 0 and res["erased"] == nerased

@@ -37,7 +37,7 @@ def test_shim_exports_every_native_method():
     src = open(os.path.join(ROOT, "lambdafs_amd", "jni", "HrsNative.java")).read()
     names = re.findall(r"static native \S+ (\w+)\(", src)
     assert {"create", "createSrc", "destroy", "locationsToRead", "encode", "decode", "decode3", "encodeCrc",
-            "decodeCrc"} <= set(names)
+            "decodeCrc", "encodeSubmit", "decodeSubmit", "collect", "pending"} <= set(names)
     lib = ctypes.CDLL(SHIM)
     for n in names:  # JNI name mangling: '_' in the package becomes '_1'
         getattr(lib, "Java_io_hops_erasure_1coding_HrsNative_" + n)
