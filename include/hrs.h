@@ -305,7 +305,7 @@ hrs_status hrs_crc32_dev(hrs_codec* codec, const uint8_t* const* rows, int nrows
  * crc_out[s * (k + p) + r] = CRC32 of data row r (r < k) or of parity row r - k
  * (r >= k) of stripe s, continuing from crc_in (same layout; NULL = fresh).
  * rs / nrs codes with a compile-time kernel ((10,4), (6,3), (3,2), (12,4) rs;
- * (10,4), (6,3) nrs), len a multiple of 32 KiB and 16-byte-aligned rows take
+ * (10,4), (6,3) nrs), len a multiple of 2 KiB and 16-byte-aligned rows take
  * one fused kernel (each cell read once); anything else runs hrs_encode_dev
  * then the CRC pass, with identical results. Asynchronous on `stream`. */
 hrs_status hrs_encode_crc_dev(hrs_codec* codec, const uint8_t* const* in_rows, size_t in_stride,
@@ -315,7 +315,7 @@ hrs_status hrs_encode_crc_dev(hrs_codec* codec, const uint8_t* const* in_rows, s
 /* Kernel selection for tests and benchmarks: 0 = auto (default), 1 = force
  * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel,
  * 3 = auto, except that hrs_encode_crc_dev takes the fused kernel whenever the
- * shape allows it, however few windows the batch has. */
+ * shape allows it. */
 hrs_status hrs_set_kernel_mode(hrs_codec* codec, int mode);
 
 #ifdef __cplusplus

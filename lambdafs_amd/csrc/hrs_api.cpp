@@ -43,6 +43,7 @@ struct hrs_codec {
   std::map<std::vector<int>, std::vector<uint8_t>> decode_cache;
   // CRC-32 state (hrs_crc32_dev): fixed window tables, per-length fold tables, scratch
   uint32_t* crc_tables_a = nullptr;
+  uint32_t* crc_tables_c = nullptr;  // the contiguous-lane fused variant's image
   std::map<uint64_t, uint32_t*> crc_fold_tables;
   uint32_t* crc_raw = nullptr;
   size_t crc_raw_bytes = 0;
@@ -1018,18 +1019,21 @@ hrs_status crc_window_tables(hrs_codec* c) {
   return crc_image(c, hrs::crc::kPieceBytes, hrs::crc::kChunkBytes, &c->crc_tables_a);
 }
 
-hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, const uint32_t** out) {
-  auto it = c->crc_fold_tables.find(len);
+// Fold tables for rows of `len` bytes cut in windows of `win` bytes (32 KiB,
+// or a smaller fused window), keyed by (len, win).
+hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, uint64_t win, const uint32_t** out) {
+  const uint64_t key = len << 5 | static_cast<uint64_t>(__builtin_ctzll(win));
+  auto it = c->crc_fold_tables.find(key);
   if (it != c->crc_fold_tables.end()) {
     *out = it->second;
     return HRS_OK;
   }
   namespace cr = hrs::crc;
-  const uint64_t nwin = len / hrs::kCrcWindow, tail = len % hrs::kCrcWindow;
+  const uint64_t nwin = len / win, tail = len % win;
   const uint64_t G = (nwin + 63) / 64;
   std::vector<uint32_t> h(hrs::kCrcLdsWordsB);
-  cr::to_tables(cr::zeros(hrs::kCrcWindow), &h[0]);
-  for (int t = 0; t < 6; ++t) cr::to_tables(cr::zeros(hrs::kCrcWindow * G << t), &h[(1 + t) * 1024]);
+  cr::to_tables(cr::zeros(win), &h[0]);
+  for (int t = 0; t < 6; ++t) cr::to_tables(cr::zeros(win * G << t), &h[(1 + t) * 1024]);
   cr::to_tables(cr::zeros(tail), &h[7 * 1024]);
   cr::to_tables(cr::zeros(len), &h[8 * 1024]);
   if (c->crc_fold_tables.size() >= 16) {
@@ -1040,7 +1044,7 @@ hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, const uint32_t** out) {
   uint32_t* d = nullptr;
   hrs_status st = upload(c, h, &d);
   if (st != HRS_OK) return st;
-  c->crc_fold_tables[len] = d;
+  c->crc_fold_tables[key] = d;
   *out = d;
   return HRS_OK;
 }
@@ -1086,16 +1090,17 @@ hrs_status crc_scratch_release(hrs_codec* c, hipStream_t s, hrs_status st) {
   return st;
 }
 
-// Folds the raw window CRCs of nsr (stripe, row) pairs into CRC32 values.
+// Folds the raw window CRCs (windows of `win` bytes) of nsr (stripe, row)
+// pairs into CRC32 values.
 hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s,
-                    uint32_t* raw) {
+                    uint32_t* raw, uint64_t win = hrs::kCrcWindow) {
   const uint32_t* fold = nullptr;
-  hrs_status st = crc_fold_tables(c, len, &fold);
+  hrs_status st = crc_fold_tables(c, len, win, &fold);
   if (st != HRS_OK) return st;
   hrs::CrcFoldArgs f{};
   f.raw = raw;
-  f.nwin = len / hrs::kCrcWindow;
-  f.tail = len % hrs::kCrcWindow;
+  f.nwin = len / win;
+  f.tail = len % win;
   f.nsr = nsr;
   f.G = static_cast<int>((f.nwin + 63) / 64);
   f.tables = fold;
@@ -1106,10 +1111,27 @@ hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_
   return HRS_OK;
 }
 
+// Sub-windows (2 KiB) per fused window: 16 (32 KiB) when the job has
+// kFusedWavesPerCU waves per CU at that size, else the largest smaller power
+// of two that does (down to 1: a job with fewer 2 KiB sub-windows than that
+// takes one wave per sub-window). 0: len is not a multiple of 2 KiB.
+constexpr uint64_t kFusedWavesPerCU = 8;
+
+uint32_t fused_subs(size_t len, size_t nstripes) {
+  if (len == 0 || len % hrs::kWindowBytes) return 0;
+  const uint64_t want = kFusedWavesPerCU * static_cast<uint64_t>(hrs::device_cu_count());
+  uint32_t subs = 16;
+  while (subs > 1 && (len % (subs * hrs::kWindowBytes) || nstripes * (len / (subs * hrs::kWindowBytes)) < want))
+    subs >>= 1;
+  return subs;
+}
+
 // Bytes of raw window-CRC scratch a CRC pass over nrows rows of nstripes
-// stripes needs (one word per 32 KiB window, the tail window included).
+// stripes needs: one word per window, the tail window included, at the
+// smallest window any pass may use (a fused 2 KiB window), so the size holds
+// for any shorter row or smaller job sized by it.
 size_t crc_raw_bytes_for(size_t len, size_t nstripes, int nrows) {
-  const uint64_t wpr = len / hrs::kCrcWindow + (len % hrs::kCrcWindow ? 1 : 0);
+  const uint64_t wpr = (len + hrs::kWindowBytes - 1) / hrs::kWindowBytes;
   return std::max<size_t>(4, nstripes * static_cast<size_t>(nrows) * wpr * 4);
 }
 
@@ -1154,18 +1176,14 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
                            size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
                            hipStream_t s, uint32_t* raw) {
   const int k = c->k, p = c->p, n = c->n;
-  // one pass: a static (k, p) of rs / nrs, whole 32 KiB windows, 16-byte aligned rows
+  // one pass: a static (k, p) of rs / nrs, whole 2 KiB sub-windows, 16-byte aligned rows.
+  // A wave walks its window's sub-windows serially over k + p rows (~20 us
+  // per 2 KiB sub-window at RS(10,4)), so jobs with few 32 KiB windows take
+  // smaller windows (fused_subs) instead of leaving CUs idle.
+  const uint32_t subs = fused_subs(len, nstripes);
   bool fused = (c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS) && (c->kernel_mode == 0 || c->kernel_mode == 3) &&
-               len > 0 &&
-               len % hrs::kCrcWindow == 0 && k <= hrs::kFusedMaxK && p <= hrs::kFusedMaxP &&
-               in_stride % 16 == 0 && out_stride % 16 == 0;
-  // The fused kernel runs one wave per (stripe, 32 KiB window), each wave
-  // serial over its k + p rows (~340 us per wave at RS(10,4)). Below ~8
-  // windows per CU that latency is the whole launch and the two bandwidth-
-  // bound passes finish first (a 512 KiB host-path chunk: 16 windows, 340 us
-  // fused vs ~40 us encode + CRC; profiles/r01/host_crc).
-  if (c->kernel_mode != 3)  // 3: take the fused kernel whenever the shape allows (tests)
-    fused &= nstripes * (len / hrs::kCrcWindow) >= 8ull * static_cast<uint64_t>(hrs::device_cu_count());
+               subs > 0 && k <= hrs::kFusedMaxK && p <= hrs::kFusedMaxP && in_stride % 16 == 0 &&
+               out_stride % 16 == 0;
   for (int i = 0; i < k && fused; ++i) fused &= aligned16(in_rows[i]);
   for (int o = 0; o < p && fused; ++o) fused &= aligned16(out_rows[o]);
   if (fused) {
@@ -1176,7 +1194,8 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
     for (int o = 0; o < p; ++o) a.out[o] = out_rows[o];
     a.in_stride = in_stride;
     a.out_stride = out_stride;
-    a.nwin = len / hrs::kCrcWindow;
+    a.subs = subs;
+    a.nwin = len / (subs * hrs::kWindowBytes);
     a.nstripes = nstripes;
     a.raw = raw;
     a.tables = c->crc_tables_a;
@@ -1184,7 +1203,7 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
     const int family = c->kind == HRS_CODE_NRS ? hrs::kStaticCauchy : hrs::kStaticRs;
     hipError_t e = hrs::launch_encode_crc(family, k, p, a, hrs::device_cu_count(), s, &handled);
     if (e != hipSuccess) return hip_fail(c, e, "fused encode+crc launch");
-    if (handled) return crc_fold(c, len, nstripes * n, crc_in, crc_out, s, raw);
+    if (handled) return crc_fold(c, len, nstripes * n, crc_in, crc_out, s, raw, subs * hrs::kWindowBytes);
   }
   // two passes: encode, then the CRC of the k sources and p parities
   hrs_status st = run_apply(c, c->g.data(), p, k, in_rows, in_stride, out_rows, out_stride, len, nstripes, s,

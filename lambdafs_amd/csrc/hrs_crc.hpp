@@ -50,11 +50,13 @@ struct CrcFoldArgs {
 hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStream_t s);
 hipError_t launch_crc_fold(const CrcFoldArgs& a, int cus, hipStream_t s);
 
-// Fused encode + CRC-32 (hrs_fused.hip): one wave per (stripe, 32 KiB
-// window) encodes the window's 16 sub-windows of 2 KiB and keeps the raw CRC
-// of every data and parity row of the window, in the window kernel's exact
-// decomposition, so crc_fold_kernel finishes them. Raw layout
-// [stripe][row][window], rows = [data 0..k-1, parity 0..p-1].
+// Fused encode + CRC-32 (hrs_fused.hip): one wave per (stripe, window of
+// `subs` 2 KiB sub-windows: 32 KiB for large jobs, smaller when a job has too
+// few 32 KiB windows to fill the chip) encodes the window's sub-windows and
+// keeps the raw CRC of every data and parity row of the window, in the window
+// kernel's decomposition (lane pieces joined with Z_1024, lanes with
+// Z_{16*2^t}), so crc_fold_kernel finishes them with Z_window tables. Raw
+// layout [stripe][row][window], rows = [data 0..k-1, parity 0..p-1].
 constexpr int kFusedMaxK = 16;
 constexpr int kFusedMaxP = 4;
 struct EncodeCrcArgs {
@@ -62,8 +64,10 @@ struct EncodeCrcArgs {
   uint8_t* out[kFusedMaxP];
   uint64_t in_stride;
   uint64_t out_stride;
-  uint64_t nwin;      // 32 KiB windows per row (len / kCrcWindow, len a multiple)
+  uint64_t nwin;      // windows per row (len / (subs * 2 KiB), len a multiple)
   uint64_t nstripes;
+  uint32_t subs;      // 2 KiB sub-windows per window: 1, 2, 4, 8 or 16
+  uint32_t pad_;
   uint32_t* raw;
   const uint32_t* tables;  // kCrcLdsWordsA words (device)
 };

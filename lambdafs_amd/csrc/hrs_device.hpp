@@ -101,6 +101,8 @@ __device__ __forceinline__ uint64_t uniform_addr(const void* p) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// The lane's two 16-byte pieces of a 2 KiB sub-window: base + loff and
+// 1 KiB later.
 __device__ __forceinline__ void load_row_u(const uint8_t* base, uint32_t loff, uint32_t (&w)[8]) {
   const g_u32x4* b = reinterpret_cast<const g_u32x4*>(uniform_addr(base) + loff);
   const u32x4 x = __builtin_nontemporal_load(b);

@@ -6,8 +6,10 @@
 // hrs_crc32_dev) the cells are read twice; fused, the CRC consumes the words
 // the encode already holds in registers.
 //
-// Decomposition: one wave per (stripe, 32 KiB window). The window is walked
-// as 16 sub-windows of 2 KiB — exactly the encode kernels' task (lane l holds
+// Decomposition: one wave per (stripe, window); a window is `subs` sub-windows
+// of 2 KiB (16 = 32 KiB for large jobs; fewer when the job has too few
+// 32 KiB windows to give every CU waves) — a sub-window is exactly the encode
+// kernels' task (lane l holds
 // the 16-byte pieces at 16 l and 1024 + 16 l of each sub-window, i.e. chunks
 // 2i and 2i+1 of the window), so the CRC decomposition is identical to
 // crc_window_kernel's (lane l owns the piece at 1024 q + 16 l of every chunk
@@ -25,8 +27,6 @@
 namespace hrs {
 namespace {
 
-constexpr int kSubWindows = kCrcWindow / kWindowBytes;  // 16
-
 template <int K, int P, class MATRIX, int THREADS>
 __global__ void __launch_bounds__(THREADS) encode_crc_kernel(const EncodeCrcArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -42,13 +42,13 @@ __global__ void __launch_bounds__(THREADS) encode_crc_kernel(const EncodeCrcArgs
   for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
     const uint64_t stripe = t / a.nwin;
     const uint64_t w = t - stripe * a.nwin;
-    const uint64_t in_base = stripe * a.in_stride + w * kCrcWindow;
-    const uint64_t out_base = stripe * a.out_stride + w * kCrcWindow;
+    const uint64_t in_base = stripe * a.in_stride + w * a.subs * kWindowBytes;
+    const uint64_t out_base = stripe * a.out_stride + w * a.subs * kWindowBytes;
     uint32_t crc[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) crc[r] = 0u;  // Z(0) = 0: the first piece needs no special case
 #pragma unroll 1
-    for (int sub = 0; sub < kSubWindows; ++sub) {
+    for (uint32_t sub = 0; sub < a.subs; ++sub) {
       const uint64_t off = static_cast<uint64_t>(sub) * kWindowBytes;
       uint32_t acc[P][8];
       uint32_t pend[P][8];
@@ -161,13 +161,13 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
   for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
     const uint64_t stripe = t / a.nwin;
     const uint64_t w = t - stripe * a.nwin;
-    const uint64_t in_base = stripe * a.in_stride + w * kCrcWindow;
-    const uint64_t out_base = stripe * a.out_stride + w * kCrcWindow;
+    const uint64_t in_base = stripe * a.in_stride + w * a.subs * kWindowBytes;
+    const uint64_t out_base = stripe * a.out_stride + w * a.subs * kWindowBytes;
     uint32_t crc[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) crc[r] = 0u;
 #pragma unroll 1
-    for (int sub = 0; sub < kSubWindows; ++sub) {
+    for (uint32_t sub = 0; sub < a.subs; ++sub) {
       const uint64_t off = static_cast<uint64_t>(sub) * kWindowBytes;
       uint32_t acc[P][8];
 #pragma unroll

@@ -6,10 +6,10 @@ readBufs, encodeBulk, parityChecksums over writeBufs), in one pass.
 Parity is checked against the engine's own encode (itself pinned to the
 oracle in test_gpu_parity.py) and, on sampled stripes, against the oracle
 directly; CRCs against zlib.crc32 (the JDK's CRC32 is zlib's CRC-32). Both the
-fused kernel (static shapes, 32 KiB-multiple cells; kernel mode 3 forces it
-on small batches) and the two-pass fallback (other shapes, ragged cells,
-unaligned rows, forced runtime kernel, batches of fewer than 8 windows per CU
-in auto mode) are covered."""
+fused kernel (static shapes, 2 KiB-multiple cells; large jobs in 32 KiB
+windows, small ones in windows of 1-8 sub-windows of 2 KiB) and the two-pass
+fallback (other shapes, ragged cells, unaligned rows, forced runtime kernel)
+are covered."""
 import zlib
 
 import numpy as np
@@ -111,7 +111,7 @@ def test_fused_chaining_like_CRC32_update(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["ragged", "shape", "forced_runtime", "unaligned", "small_batch"])
+@pytest.mark.parametrize("case", ["ragged", "shape", "forced_runtime", "unaligned"])
 def test_two_pass_fallback(cuda, case):
     torch = cuda
     k, p, L, S = 10, 4, 96 << 10, 3
@@ -150,3 +150,26 @@ def test_fused_crc_in_layout_and_errors(cuda):
     crc = device.encode_stripes_crc(code, st, cin)
     torch.cuda.synchronize()
     _check(torch, code, st, crc, np.zeros((2, 4, 32 << 10), np.uint8), cin.cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,L", [(1, 2 << 10), (1, 6 << 10), (2, 34 << 10), (1, 512 << 10), (1, 1 << 20),
+                                 (7, 192 << 10), (64, 256 << 10), (300, 64 << 10)])
+def test_fused_window_sizes(cuda, S, L):
+    """The fused kernel's window choice (1..16 sub-windows of 2 KiB, by how
+    many waves the job gives each CU): the Encoder's single-stripe 512 KiB /
+    1 MiB rounds, odd sub-window counts, many small stripes. Parity vs the
+    engine's encode (pinned to the oracle), CRCs vs zlib, continued from a
+    running value."""
+    torch = cuda
+    k, p = 10, 4
+    code = HipReedSolomonCode(k, p)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(S * 7 + L)
+    st = torch.randint(0, 256, (S, k + p, L), dtype=torch.uint8, device="cuda", generator=g)
+    ref = _reference_parity(torch, code, st)
+    st[:, :p] = 0xA5
+    cin = torch.randint(-2**31, 2**31 - 1, (S, k + p), dtype=torch.int32, device="cuda", generator=g)
+    crc = device.encode_stripes_crc(code, st, cin)
+    torch.cuda.synchronize()
+    _check(torch, code, st, crc, ref, cin.cpu().numpy())
