@@ -9,7 +9,7 @@ CC       ?= gcc
 LIB      := lambdafs_amd/libhrs.so
 ORACLE   := oracle/liboracle.so
 HDRS     := Makefile include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
-            lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
+            lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp lambdafs_amd/csrc/xor_sched.hpp
 
 JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic

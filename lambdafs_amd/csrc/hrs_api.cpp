@@ -43,7 +43,6 @@ struct hrs_codec {
   std::map<std::vector<int>, std::vector<uint8_t>> decode_cache;
   // CRC-32 state (hrs_crc32_dev): fixed window tables, per-length fold tables, scratch
   uint32_t* crc_tables_a = nullptr;
-  uint32_t* crc_tables_c = nullptr;  // the contiguous-lane fused variant's image
   std::map<uint64_t, uint32_t*> crc_fold_tables;
   uint32_t* crc_raw = nullptr;
   size_t crc_raw_bytes = 0;

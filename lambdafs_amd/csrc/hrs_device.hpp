@@ -5,10 +5,12 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "gf256.hpp"
 #include "hrs_crc.hpp"
 #include "hrs_internal.hpp"
+#include "xor_sched.hpp"
 
 namespace hrs {
 
@@ -162,6 +164,64 @@ __device__ __forceinline__ void encode_row_acc(int r, const uint32_t (&w)[8], ui
         }
       }
     }
+}
+
+// ------------------------------------------- factored XOR networks (CSE)
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Schedule family of a compile-time matrix (xor_sched.hpp): 0 = hops RS
+// generator rows, 1 = ISA-L Cauchy rows.
+template <class MATRIX> struct MatrixFamily;
+template <int K, int P> struct MatrixFamily<gf::EncodeMatrix<K, P>> { static constexpr int value = 0; };
+template <int K, int P> struct MatrixFamily<gf::CauchyMatrix<K, P>> { static constexpr int value = 1; };
+
+// Group GI of a factored schedule (tools/gen_xor_sched.py): the group's
+// sliced input planes x[g][i] are vars 8g + i; the shared temporaries are
+// built first (one xor3 or XOR each), then every parity plane folds in its
+// remaining terms two per xor3. Group 0 starts the planes (no running
+// value). Every index is a compile-time constant, so v[] lives in registers.
+// RS(10,4): 290-386 xor ops per 2 KiB window instead of 631-660 plane by
+// plane, depending on the rows per group.
+template <class S, int GI, int G, int P>
+__device__ __forceinline__ void xor_sched_apply(const uint32_t (&x)[G][8], uint32_t (&acc)[P][8]) {
+  constexpr int nin = S::kNin[GI];
+  constexpr int op0 = S::kOpOff[GI];
+  constexpr int nops = S::kOpOff[GI + 1] - op0;
+  uint32_t v[S::kMaxVars];
+#pragma unroll
+  for (int i = 0; i < nin; ++i) v[i] = x[i >> 3][i & 7];
+  static_for<0, nops>([&](auto j) __attribute__((always_inline)) {
+    constexpr xsched::Op op = S::kOps[op0 + decltype(j)::value];
+    if constexpr (op.c == 255)
+      v[nin + decltype(j)::value] = v[op.a] ^ v[op.b];
+    else
+      v[nin + decltype(j)::value] = xor3(v[op.a], v[op.b], v[op.c]);
+  });
+  static_for<0, 8 * P>([&](auto pl) __attribute__((always_inline)) {
+    constexpr int t0 = S::kTermOff[GI][decltype(pl)::value];
+    constexpr int t1 = S::kTermOff[GI][decltype(pl)::value + 1];
+    uint32_t& a = acc[decltype(pl)::value >> 3][decltype(pl)::value & 7];
+    int t = t0;
+    if constexpr (GI == 0) {
+      if constexpr (t1 == t0) {
+        a = 0u;
+      } else {
+        a = v[S::kTerms[t0]];
+        t = t0 + 1;
+      }
+    }
+#pragma unroll
+    for (; t + 1 < t1; t += 2) a = xor3(a, v[S::kTerms[t]], v[S::kTerms[t + 1]]);
+    if (t < t1) a ^= v[S::kTerms[t]];
+  });
 }
 
 // ------------------------------------------------------------ CRC-32 steps

@@ -140,17 +140,22 @@ __device__ __forceinline__ void encode_group_acc(int r0, const uint32_t (&x)[G][
 // lockstep (8G independent LDS lookups per slicing step), each running CRC is
 // pinned in place as soon as it is updated (otherwise the compiler sinks its
 // final XORs to the loop end and keeps every row's table words live:
-// spills), and the group's planes are paired into xor3s across its rows (an
-// odd leftover costs one XOR per group, not per row). The next word of a
-// piece folds into each slicing step's XOR tree (slice4_xor), the Horner
-// term into the zmul's (zmul_xor). Per 2 KiB sub-window of RS(10,4): 2,313
-// VALU (row-serial: 2,473). G need not divide K (a last, smaller group).
-template <int K, int P, class MATRIX, int THREADS, int G>
+// spills). The next word of a piece folds into each slicing step's XOR tree
+// (slice4_xor), the Horner term into the zmul's (zmul_xor). G need not divide
+// K (a last, smaller group).
+// Parity: SCHED (the default) evaluates the group's factored XOR network
+// (xor_sched.hpp: shared xor3 temporaries over the group's 8G planes), else
+// each plane's selected planes are paired into xor3s across the group's rows.
+// Per 2 KiB sub-window of RS(10,4), G = 2: 2,048 VALU factored, 2,313 paired
+// (row-serial: 2,473); measured 3.10 vs 3.17 ms (RS(12,4), G = 4: 3.60 vs
+// 3.92 ms), profiles/r02/sched.
+template <int K, int P, class MATRIX, int THREADS, int G, bool SCHED>
 __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const EncodeCrcArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   for (int i = threadIdx.x; i < kCrcLdsWordsA; i += THREADS) lds[i] = a.tables[i];
   __syncthreads();
   constexpr int N = K + P;
+  constexpr int kGroups = (K + G - 1) / G;
   const int lane = threadIdx.x & 63;
   const uint32_t loff = static_cast<uint32_t>(lane) * 16u;
   const SliceTab slices = slice_tab(lane);
@@ -170,12 +175,15 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
     for (uint32_t sub = 0; sub < a.subs; ++sub) {
       const uint64_t off = static_cast<uint64_t>(sub) * kWindowBytes;
       uint32_t acc[P][8];
+      if constexpr (!SCHED) {
 #pragma unroll
-      for (int o = 0; o < P; ++o)
+        for (int o = 0; o < P; ++o)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
-#pragma unroll
-      for (int r0 = 0; r0 < K; r0 += G) {
+          for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+      }
+      static_for<0, kGroups>([&](auto gi) __attribute__((always_inline)) {
+        constexpr int GI = decltype(gi)::value;
+        constexpr int r0 = GI * G;
         HRS_PHASE_FENCE();
         uint32_t x[G][8];
 #pragma unroll
@@ -210,8 +218,11 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
 #pragma unroll
         for (int g = 0; g < G; ++g)
           if (r0 + g < K) bitslice(x[g]);
-        encode_group_acc<K, P, MATRIX, G>(r0, x, acc);
-      }
+        if constexpr (SCHED)
+          xor_sched_apply<xsched::Sched<MatrixFamily<MATRIX>::value, K, P, G>, GI, G, P>(x, acc);
+        else
+          encode_group_acc<K, P, MATRIX, G>(r0, x, acc);
+      });
       HRS_PHASE_FENCE();
 #pragma unroll
       for (int o = 0; o < P; ++o) {
@@ -233,49 +244,66 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
 
 // One 1024-thread block per CU (16 waves share the 156 KiB table image).
 constexpr int kFusedThreads = 1024;
-constexpr int kFusedGroupDefault = 2;  // measured best (profiles/r02/fused/)
 
-int fused_variant() {  // HRS_FUSED=1: the row-serial form (A/B runs)
+// Rows per lockstep group, measured best (profiles/r02/sched): 2 (RS(10,4)
+// 3.10 ms vs 3.06-3.28 at 4), 4 from K = 12 (RS(12,4) 3.60 vs 3.72 at 2).
+template <int K>
+constexpr int kFusedGroup = K >= 12 ? 4 : 2;
+
+// HRS_FUSED (A/B runs): 1 = row-serial, 2 = grouped with the paired XOR
+// network, default = grouped with the factored network. HRS_FUSED_GROUP
+// overrides the rows per group (1 | 2 | 4).
+int fused_variant() {
   static const int v = [] {
     const char* e = getenv("HRS_FUSED");
-    return e && e[0] == '1' ? 1 : 2;
+    if (e && e[0] == '1') return 1;
+    if (e && e[0] == '2') return 2;
+    return 3;
   }();
   return v;
 }
 
-int fused_group() {  // HRS_FUSED_GROUP: rows per lockstep group (A/B runs)
+int fused_group() {
   static const int v = [] {
     const char* e = getenv("HRS_FUSED_GROUP");
     const int x = e ? atoi(e) : 0;
-    return (x == 1 || x == 2 || x == 4) ? x : kFusedGroupDefault;
+    return (x == 1 || x == 2 || x == 4) ? x : 0;
   }();
   return v;
 }
 
 using CrcKernel = void (*)(const EncodeCrcArgs);
+struct CrcPick {
+  CrcKernel k;
+  int threads;
+};
 
 template <int K, int P, class MATRIX>
-CrcKernel pick_kernel() {
-  if (fused_variant() == 1) return encode_crc_kernel<K, P, MATRIX, kFusedThreads>;
-  const int g = fused_group();
-  if (g == 4) return encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 4>;
-  if (g == 1) return encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 1>;
-  return encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2>;
+CrcPick pick_kernel() {
+  if (fused_variant() == 1) return {encode_crc_kernel<K, P, MATRIX, kFusedThreads>, kFusedThreads};
+  const int g = fused_group() ? fused_group() : kFusedGroup<K>;
+  if (fused_variant() == 3) {  // factored XOR network (xor_sched.hpp has G = 2, min(4, K), K)
+    if (g == 4) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, (K > 4 ? 4 : K), true>, kFusedThreads};
+    return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2, true>, kFusedThreads};
+  }
+  if (g == 4) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 4, false>, kFusedThreads};
+  if (g == 1) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 1, false>, kFusedThreads};
+  return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2, false>, kFusedThreads};
 }
 
 template <int K, int P, class MATRIX>
 hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
   const uint64_t ntasks = a.nstripes * a.nwin;
-  const CrcKernel k = pick_kernel<K, P, MATRIX>();
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+  const CrcPick k = pick_kernel<K, P, MATRIX>();
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k.k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;
-  const uint64_t per_block = kFusedThreads / 64;
+  const uint64_t per_block = k.threads / 64;
   uint64_t g = (ntasks + per_block - 1) / per_block;
   if (g > static_cast<uint64_t>(cus)) g = cus;
   if (g == 0) g = 1;
-  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kFusedThreads), shm, s, a);
+  hipLaunchKernelGGL(k.k, dim3(static_cast<unsigned>(g)), dim3(k.threads), shm, s, a);
   return hipGetLastError();
 }
 
