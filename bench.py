@@ -40,7 +40,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU (weak scaling)")
     ap.add_argument("--strong", action="store_true",
@@ -511,7 +511,7 @@ def main():
             },
             "encode_crc": {
                 "what": "encode + java.util.zip.CRC32 of all k+p cells (Encoder with computeBlockChecksum)",
-                "kernel": f"encode_crc_grouped_kernel<{k},{p},G=2> + crc_fold_kernel",
+                "kernel": f"encode_crc_grouped_kernel<{k},{p},G={4 if k >= 12 else 2},factored> + crc_fold_kernel",
                 "fused_ms": stats(fused_ms),
                 "two_pass_ms": stats(two_ms),
                 "fused_GBps_algorithmic": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9, 1),
@@ -524,7 +524,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
-            res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 12, threads=1)
+            res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 40, threads=1)
             res["cpu_baseline"]["gpu_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
     if world > 1:
