@@ -8,7 +8,7 @@ CC       ?= gcc
 
 LIB      := lambdafs_amd/libhrs.so
 ORACLE   := oracle/liboracle.so
-HDRS     := Makefile include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
+HDRS     := Makefile include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/hrs_launch.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
             lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp lambdafs_amd/csrc/xor_sched.hpp
 
 JNI      := lambdafs_amd/libhrs_jni.so
@@ -24,6 +24,14 @@ build/hrs_kernels.o: lambdafs_amd/csrc/hrs_kernels.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+build/hrs_runtime.o: lambdafs_amd/csrc/hrs_runtime.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/hrs_batch.o: lambdafs_amd/csrc/hrs_batch.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 build/hrs_crc.o: lambdafs_amd/csrc/hrs_crc.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -35,7 +43,9 @@ build/hrs_fused.o: lambdafs_amd/csrc/hrs_fused.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -mllvm -pragma-unroll-threshold=1000000 -c $< -o $@
 
-$(LIB): build/hrs_api.o build/hrs_kernels.o build/hrs_crc.o build/hrs_fused.o
+KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o
+
+$(LIB): build/hrs_api.o $(KOBJ)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
@@ -82,7 +92,7 @@ $(ASAN_DIR)/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS) lambdafs_amd/csrc/h
 	@mkdir -p $(ASAN_DIR)
 	$(HIPCC) -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) $(HSAN) -x hip -c $< -o $@
 
-$(ASAN_DIR)/libhrs.so: $(ASAN_DIR)/hrs_api.o build/hrs_kernels.o build/hrs_crc.o build/hrs_fused.o
+$(ASAN_DIR)/libhrs.so: $(ASAN_DIR)/hrs_api.o $(KOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -fsanitize=address,undefined -o $@ $^
 
 $(ASAN_DIR)/liboracle.so: oracle/rs_oracle.c oracle/rs_oracle.h

@@ -327,4 +327,27 @@ __device__ __forceinline__ uint32_t lane_tree(const uint32_t* tree, uint32_t c) 
   return c;
 }
 
+// ---------------------------------------- runtime-matrix kernel helpers
+
+// NINB >= nin rows of the window are all loaded before any math (one
+// 20 KiB-class burst per wave, like the static kernel), so a wave keeps
+// nin x 2 KiB in flight; coefficients are wave-uniform kernel arguments.
+// Bit loop unrolled (xtime is then a free relabel of the planes) unless the
+// body would outgrow the instruction cache: unrolled, bitsliced<4,12> is
+// 28 KiB of branchy code and ran 40% slower than rolled.
+template <int NOUT, int NINB>
+struct BitLoop {
+  static constexpr bool kRolled = NOUT * NINB >= 40;
+};
+
+template <int NOUT, int NINB>
+__device__ __forceinline__ void mul_acc_row(uint32_t (&acc)[NOUT][8], uint32_t (&x)[8], const uint32_t (&cw)[2], int b) {
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o)
+    if ((cw[o >> 2] >> (8 * (o & 3) + b)) & 1u) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] ^= x[q];
+    }
+}
+
 }  // namespace hrs

@@ -1,0 +1,67 @@
+// Host-side launch geometry shared by the kernel translation units
+// (hrs_kernels.hip, hrs_runtime.hip, hrs_batch.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstdlib>
+
+#include "hrs_internal.hpp"
+
+namespace hrs {
+
+
+// CU count per device, cached; handles on several host threads may race to
+// fill it (same value), hence the relaxed atomics.
+inline int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  static std::atomic<int> cus_of[64];
+  if (dev < 0 || dev >= 64) return 256;
+  int cus = cus_of[dev].load(std::memory_order_relaxed);
+  if (cus == 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cus_of[dev].store(cus, std::memory_order_relaxed);
+  }
+  return cus;
+}
+
+// Streaming kernels: a fixed number of resident blocks per CU, grid-striding
+// over the tasks. 2 x 256-thread blocks per CU (8 waves, each with a whole
+// window's rows in flight) measured fastest for both the static and the
+// runtime kernels (tools/kernel_lab.hip sweep, 256..1024 blocks); override
+// with HRS_BLOCKS_PER_CU for experiments.
+// VALU-bound shapes (the rolled bit loop: 3-4 erasure repairs, wide
+// matrices) take 3 blocks per CU: the extra wave per SIMD hides more of the
+// math (RS(10,4) 4-erasure decode +13%, profiles/r01/pipe/).
+inline int blocks_per_cu(int dflt = 2) {
+  static int v = [] {
+    const char* e = getenv("HRS_BLOCKS_PER_CU");
+    int x = e ? atoi(e) : 0;
+    return (x >= 1 && x <= 32) ? x : 0;
+  }();
+  return v ? v : dflt;
+}
+
+inline unsigned stream_grid(uint64_t ntasks, int per_cu = 2) {
+  const uint64_t want = static_cast<uint64_t>(blocks_per_cu(per_cu)) * device_cus();
+  const uint64_t needed = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+  uint64_t g = needed < want ? needed : want;
+  return static_cast<unsigned>(g == 0 ? 1 : g);
+}
+
+template <typename Kernel>
+inline unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t ntasks) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockThreads, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 2;
+  const uint64_t resident = static_cast<uint64_t>(per_cu) * device_cus();
+  const uint64_t needed = (ntasks + work_items_per_block - 1) / work_items_per_block;
+  uint64_t g = needed < resident ? needed : resident;
+  if (g == 0) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+}  // namespace hrs

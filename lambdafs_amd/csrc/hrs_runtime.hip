@@ -1,0 +1,210 @@
+// gfx950 runtime-matrix kernels: decode (and the encode of codes without a
+// compile-time kernel) as out = M * in with the coefficients of M in the
+// kernel arguments — bit-sliced rows, planes multiplied by alpha and
+// accumulated under wave-uniform branches (see hrs_kernels.hip's header for
+// the arithmetic; bitslice / xtime / mul_acc_row in hrs_device.hpp).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "hrs_device.hpp"
+#include "hrs_launch.hpp"
+
+namespace hrs {
+namespace {
+
+template <int NOUT, int NINB>
+__global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
+    asm volatile("" : "+s"(nin));
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t rows[NINB][8];
+#pragma unroll
+    for (int r = 0; r < NINB; ++r)
+      if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
+    uint32_t acc[NOUT][8];
+    if (a.accumulate) {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) {
+        load_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+        bitslice(acc[o]);
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < NINB; ++r) {
+      if (r < nin) {
+        bitslice(rows[r]);
+        // one wave-uniform 64-bit word per input (byte o = coefficient of
+        // output o), split in halves; the empty asm keeps the per-(o, b)
+        // tests from being hoisted out of the task loop (they would spill).
+        uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
+        asm volatile("" : "+s"(cw[0]));
+        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
+        // acc[o] ^= sum over set bits b of coef[o][r]: alpha^b * row
+        if constexpr (BitLoop<NOUT, NINB>::kRolled) {
+#pragma unroll 1
+          for (int b = 0; b < 8; ++b) {
+            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+            xtime(rows[r]);
+          }
+        } else {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+            if (b < 7) xtime(rows[r]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      bitslice(acc[o]);
+      store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+  }
+}
+
+// Software-pipelined form of bitsliced_kernel for narrow outputs: two
+// register sets of NINB rows, the next task's rows are loaded before the
+// current task's math, so a wave keeps a window in flight while it computes
+// (the plain kernel's loads sit idle during its ~1,000 VALU of slicing and
+// multiplying). 2*NINB*8 + 8*NOUT VGPRs: NOUT <= 2, NINB <= 12 at 2 waves/SIMD.
+template <int NOUT, int NINB>
+__device__ __forceinline__ void load_task(const RowArgs& a, uint64_t t, int nin, int lane,
+                                          uint32_t (&rows)[NINB][8]) {
+  const uint64_t stripe = t / a.nwin;
+  const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+  const uint64_t in_base = stripe * a.in_stride + off;
+#pragma unroll
+  for (int r = 0; r < NINB; ++r)
+    if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
+}
+
+template <int NOUT, int NINB>
+__device__ __forceinline__ void apply_task(const RowArgs& a, uint64_t t, int nin, int lane,
+                                           uint32_t (&rows)[NINB][8]) {
+  const uint64_t stripe = t / a.nwin;
+  const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+  uint32_t acc[NOUT][8];
+  if (a.accumulate) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      load_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+      bitslice(acc[o]);
+    }
+  } else {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < NINB; ++r) {
+    if (r < nin) {
+      bitslice(rows[r]);
+      uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
+      asm volatile("" : "+s"(cw[0]));
+        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
+        if (b < 7) xtime(rows[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    bitslice(acc[o]);
+    store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+  }
+}
+
+template <int NOUT, int NINB>
+__global__ void __launch_bounds__(kBlockThreads) bitsliced_pipe_kernel(const RowArgs a) {
+  static_assert(!BitLoop<NOUT, NINB>::kRolled, "pipelined kernel takes the unrolled shapes only");
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  int nin = a.nin;
+  asm volatile("" : "+s"(nin));
+  uint64_t t = wave_id_in_grid();
+  if (t >= a.ntasks) return;
+  uint32_t ra[NINB][8], rb[NINB][8];
+  load_task<NOUT, NINB>(a, t, nin, lane, ra);
+  for (;;) {  // every wave leaves once its next task index passes ntasks
+    const uint64_t t1 = t + nwaves;
+    if (t1 < a.ntasks) load_task<NOUT, NINB>(a, t1, nin, lane, rb);
+    apply_task<NOUT, NINB>(a, t, nin, lane, ra);
+    if (t1 >= a.ntasks) break;
+    const uint64_t t2 = t1 + nwaves;
+    if (t2 < a.ntasks) load_task<NOUT, NINB>(a, t2, nin, lane, ra);
+    apply_task<NOUT, NINB>(a, t1, nin, lane, rb);
+    if (t2 >= a.ntasks) break;
+    t = t2;
+  }
+}
+
+// Software-pipelined runtime kernel for the unrolled shapes that fit (the 1-
+// to 3-erasure repairs: RS(10,4) 1-erasure decode +3-10%, 2-3 erasures
+// neutral); HRS_PIPE=0 selects the plain kernel for A/B runs. The same
+// pipelining of the static encode (-1%) and of the heterogeneous batch
+// kernel (-2%) measured slower and is not used (profiles/r01/pipe/ab2).
+// Unrolled shapes whose two row sets + accumulators fit 2 waves/SIMD.
+template <int NOUT, int NINB>
+constexpr bool kPipeFits = !BitLoop<NOUT, NINB>::kRolled && 16 * NINB + 8 * NOUT <= 232;
+
+bool use_pipe() {
+  static bool v = [] {
+    const char* e = getenv("HRS_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+template <int NOUT, int NINB>
+hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
+  auto kern = bitsliced_kernel<NOUT, NINB>;
+  if constexpr (kPipeFits<NOUT, NINB>)
+    if (use_pipe()) kern = bitsliced_pipe_kernel<NOUT, NINB>;
+  const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NOUT>
+hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
+  if (a.nin <= 4) return launch_bits_n<NOUT, 4>(a, s);
+  if (a.nin <= 8) return launch_bits_n<NOUT, 8>(a, s);
+  if constexpr (NOUT < 6) {  // wider outputs would spill: the host chunks them by 8 inputs
+    if (a.nin <= 12) return launch_bits_n<NOUT, 12>(a, s);
+    if (a.nin <= 16) return launch_bits_n<NOUT, 16>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s) {
+  switch (a.nout) {
+    case 1: return launch_bits<1>(a, s);
+    case 2: return launch_bits<2>(a, s);
+    case 3: return launch_bits<3>(a, s);
+    case 4: return launch_bits<4>(a, s);
+    case 5: return launch_bits<5>(a, s);
+    case 6: return launch_bits<6>(a, s);
+    case 7: return launch_bits<7>(a, s);
+    case 8: return launch_bits<8>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace hrs
