@@ -13,7 +13,7 @@ except ImportError:  # pragma: no cover
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhrs.so")
+LIB_PATH = os.environ.get("HRS_LIB") or os.path.join(_HERE, "libhrs.so")  # HRS_LIB: A/B runs of another build
 
 HRS_OK = 0
 HRS_EINVAL = 1
