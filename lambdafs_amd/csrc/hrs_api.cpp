@@ -629,9 +629,24 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
     }
     return HRS_OK;
   }
+  // Shapes the register-resident kernels would take in several launches go to
+  // the streaming kernel (each input read once, each output written once, up
+  // to kMaxIn inputs per launch), and so do 13-16 inputs with 3+ outputs, where
+  // holding all 16 rows costs the resident kernel its occupancy (RS(16,4)
+  // encode 4.50 -> 3.03 ms; 1-2 outputs and <= 12 inputs stay resident, where
+  // streaming measured equal or slower: profiles/r02/stream). HRS_STREAM=0
+  // keeps the chunked launches, 2 streams every runtime-matrix launch.
+  static const int stream_mode = [] {
+    const char* e = getenv("HRS_STREAM");
+    return e ? atoi(e) : 1;
+  }();
+  const bool stream_ok = stream_mode != 0;
   for (int o0 = 0; o0 < nout; o0 += hrs::kMaxOut) {
     const int no = std::min(hrs::kMaxOut, nout - o0);
-    const int chunk = hrs::runtime_in_chunk(no);
+    const int resident = hrs::runtime_in_chunk(no);
+    const bool stream = stream_ok && mode == 0 && nwin > 0 &&
+                        (nlive > resident || (nlive > 12 && no >= 3) || stream_mode == 2);
+    const int chunk = stream ? hrs::kMaxIn : resident;
     for (int i0 = 0; i0 < nlive; i0 += chunk) {
       const int ni = std::min(chunk, nlive - i0);
       RowArgs a{};
@@ -649,7 +664,7 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
         a.len = len;
         a.nwin = nwin;
         a.ntasks = nwin * nstripes;
-        hipError_t e = hrs::launch_bitsliced(a, s);
+        hipError_t e = stream ? hrs::launch_bitsliced_stream(a, s) : hrs::launch_bitsliced(a, s);
         if (e != hipSuccess) return hip_fail(c, e, "bitsliced launch");
       }
       if (tail > 0) {

@@ -54,6 +54,7 @@ enum class KernelKind : int {
 enum { kStaticRs = 0, kStaticCauchy = 1 };
 hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipStream_t s, bool* handled);
 hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s);
+hipError_t launch_bitsliced_stream(const RowArgs& a, hipStream_t s);  // up to kMaxIn inputs, one pass
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s);
 hipError_t launch_xor(const RowArgs& a, hipStream_t s);
 int device_cu_count();  // CUs of the current device (cached)

@@ -153,6 +153,97 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_pipe_kernel(const Row
   }
 }
 
+// Streaming form for shapes the kernels above take in several launches (more
+// inputs than they hold in registers: > 16 inputs, or > 8 with 6-8 outputs),
+// whose later launches re-read and re-write every output (RS(20,8) encode moved
+// 60 rows of HBM traffic per stripe instead of 28). Here a wave walks the
+// window's inputs in groups of D rows with two register sets: group g + 1 is
+// loaded while group g is bit-sliced and accumulated, so each input row is
+// read once and each output written once for up to kMaxIn (32) inputs, and
+// the wave still keeps D rows in flight. The coefficient words and row
+// pointers of group g come from the kernel arguments by a wave-uniform index
+// (scalar loads).
+template <int NOUT, int D>
+__device__ __forceinline__ void load_group(const RowArgs& a, int r0, int nin, uint64_t in_base, int lane,
+                                           uint32_t (&rows)[D][8]) {
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (r0 + j < nin) load_row(a.in[r0 + j] + in_base, lane, rows[j]);
+}
+
+template <int NOUT, int D>
+__device__ __forceinline__ void acc_group(const RowArgs& a, int r0, int nin, uint32_t (&acc)[NOUT][8],
+                                          uint32_t (&rows)[D][8]) {
+  constexpr int kNinb = NOUT >= 4 ? 16 : 8;  // BitLoop: rolled bit loop from 4 outputs
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    if (r0 + j < nin) {
+      bitslice(rows[j]);
+      const uint64_t w = a.cw[r0 + j];
+      uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
+      asm volatile("" : "+s"(cw[0]));
+      if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));
+      if constexpr (BitLoop<NOUT, kNinb>::kRolled) {
+#pragma unroll 1
+        for (int b = 0; b < 8; ++b) {
+          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
+          xtime(rows[j]);
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
+          if (b < 7) xtime(rows[j]);
+        }
+      }
+    }
+  }
+}
+
+template <int NOUT, int D>
+__global__ void __launch_bounds__(kBlockThreads) bitsliced_stream_kernel(const RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    int nin = a.nin;
+    asm volatile("" : "+s"(nin));
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t acc[NOUT][8];
+    if (a.accumulate) {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) {
+        load_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+        bitslice(acc[o]);
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+    }
+    uint32_t ra[D][8], rb[D][8];
+    load_group<NOUT, D>(a, 0, nin, in_base, lane, ra);
+#pragma unroll 1
+    for (int r0 = 0; r0 < nin; r0 += 2 * D) {
+      if (r0 + D < nin) load_group<NOUT, D>(a, r0 + D, nin, in_base, lane, rb);
+      acc_group<NOUT, D>(a, r0, nin, acc, ra);
+      if (r0 + D >= nin) break;
+      if (r0 + 2 * D < nin) load_group<NOUT, D>(a, r0 + 2 * D, nin, in_base, lane, ra);
+      acc_group<NOUT, D>(a, r0 + D, nin, acc, rb);
+    }
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      bitslice(acc[o]);
+      store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+  }
+}
+
+// Rows per streamed group: 4 (8 rows of loads in flight per wave).
+constexpr int kStreamGroup = 4;
+
 // Software-pipelined runtime kernel for the unrolled shapes that fit (the 1-
 // to 3-erasure repairs: RS(10,4) 1-erasure decode +3-10%, 2-3 erasures
 // neutral); HRS_PIPE=0 selects the plain kernel for A/B runs. The same
@@ -191,7 +282,30 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+template <int NOUT>
+hipError_t launch_stream_n(const RowArgs& a, hipStream_t s) {
+  auto kern = bitsliced_stream_kernel<NOUT, kStreamGroup>;
+  const int per_cu = NOUT >= 4 ? 3 : 2;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_bitsliced_stream(const RowArgs& a, hipStream_t s) {
+  if (a.nin < 1 || a.nin > kMaxIn) return hipErrorInvalidValue;
+  switch (a.nout) {
+    case 1: return launch_stream_n<1>(a, s);
+    case 2: return launch_stream_n<2>(a, s);
+    case 3: return launch_stream_n<3>(a, s);
+    case 4: return launch_stream_n<4>(a, s);
+    case 5: return launch_stream_n<5>(a, s);
+    case 6: return launch_stream_n<6>(a, s);
+    case 7: return launch_stream_n<7>(a, s);
+    case 8: return launch_stream_n<8>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_bitsliced(const RowArgs& a, hipStream_t s) {
   switch (a.nout) {
