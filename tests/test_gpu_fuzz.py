@@ -6,7 +6,9 @@ cross product they sample sparsely: code family (rs / nrs / xor / src) x
 (k, p) x cell length (1 byte, 16-byte and 2 KiB window edges, 32 KiB fused
 windows, ragged) x row placement (16-byte aligned or not, padded stripe
 pitch) x entry point (device encode, device decode, heterogeneous repair
-batch, host-row encode/decode, fused encode + CRC-32). Every case uses
+batch, host-row encode/decode, fused encode + CRC-32, the host calls with
+block checksums, asynchronous submit/collect rounds, host-memory batches).
+Every case uses
 non-codeword inputs where the entry point allows it, so every coefficient of
 every matrix is exercised, and is compared bit for bit.
 
@@ -29,7 +31,7 @@ from oracle import rs_oracle as C
 
 pytestmark = pytest.mark.gpu
 
-CASES = 300
+CASES = 400
 SEED = 0x5EED_F022
 LENGTHS = [1, 15, 16, 17, 100, 2047, 2048, 2049, 4096 + 17, 32768, 65536, 32768 * 3 + 2048 + 5]
 SRC_SHAPES = [(10, 6, 2), (6, 3, 2), (10, 4, 3), (10, 4, 1), (6, 3, 1), (12, 4, 1), (3, 2, 1), (10, 4, 2)]
@@ -37,9 +39,10 @@ STATIC_RS = [(10, 4), (6, 3), (3, 2), (12, 4)]
 STATIC_NRS = [(10, 4), (6, 3)]
 
 
-ENTRIES = {"rs": ["enc", "dec", "batch", "host", "crc"], "nrs": ["enc", "dec", "host", "crc"],
-           "xor": ["enc", "dec", "host"], "src": ["enc", "dec", "batch"]}
-PAIRS = [(f, e) for f in ENTRIES for e in ENTRIES[f]]  # case i draws pair i % 15, the rest at random
+ENTRIES = {"rs": ["enc", "dec", "batch", "host", "crc", "hcrc", "async", "hbatch"],
+           "nrs": ["enc", "dec", "host", "crc", "hcrc", "async"],
+           "xor": ["enc", "dec", "host", "hcrc", "async"], "src": ["enc", "dec", "batch", "hbatch"]}
+PAIRS = [(f, e) for f in ENTRIES for e in ENTRIES[f]]  # case i draws pair i % len(PAIRS), the rest at random
 
 
 def _case(rnd, fam, entry):
@@ -223,6 +226,113 @@ def _check_crc(torch, fam, k, p, s, st, host_before):
     return S * (k + p)
 
 
+def _host_pattern_reads(fam, k, p, s, host, rnd):
+    """One decodable pattern and the reads the reference decoder sees for it."""
+    pat = None
+    while pat is None:
+        pat = _pattern(fam, k, p, s, rnd)
+    erased, ntr, tr = pat
+    reads = [None if x in ntr else host[x].copy() for x in range(k + p)]
+    if fam == "xor":
+        reads = [np.zeros_like(host[0]) if r is None else r for r in reads]
+    ref_reads = [np.zeros_like(host[0]) if (r is None and fam == "rs") else r for r in reads]
+    return erased, ntr, tr, reads, ref_reads
+
+
+def _check_hcrc(fam, k, p, s, host, rnd):
+    """encodeBulkCrc / decodeBulkCrc (the Encoder's and Decoder's block
+    checksums) with running CRCs continued from random values."""
+    L = host.shape[2]
+    code = _code(fam, k, p, s)
+    code.zero_inputs_after_encode = False
+    data = [host[0, p + c].copy() for c in range(k)]
+    par = [np.full(L, 0xA5, np.uint8) for _ in range(p)]
+    run = [rnd.randrange(1 << 32) for _ in range(k + p)]
+    got = code.encodeBulkCrc(data, par, run)
+    ref = _ref_encode(fam, k, p, s, data)
+    assert all((a == b).all() for a, b in zip(par, ref))
+    assert got == [zlib.crc32(r.tobytes(), c) for r, c in zip(data + list(ref), run)]
+    erased, ntr, tr, reads, ref_reads = _host_pattern_reads(fam, k, p, s, host[0], rnd)
+    outs = [np.full(L, 0x5A, np.uint8) for _ in erased]
+    run = [rnd.randrange(1 << 32) for _ in erased]
+    got = code.decodeBulkCrc(reads, outs, erased, tr, ntr, run)
+    want = _ref_decode(fam, k, p, s, ref_reads, erased, ntr, tr)
+    assert all((a == b).all() for a, b in zip(outs, want))
+    assert got == [zlib.crc32(w.tobytes(), c) for w, c in zip(want, run)]
+    return p + 2 * len(erased)
+
+
+def _check_async(fam, k, p, s, host, rnd):
+    """Asynchronous rounds: every stripe submitted (encode, then a decode of
+    a fresh pattern) before any is collected, collected out of order."""
+    L, S = host.shape[2], host.shape[0]
+    code = _code(fam, k, p, s)
+    code.zero_inputs_after_encode = False
+    subs = []
+    for i in range(min(S, 2)):
+        data = [host[i, p + c].copy() for c in range(k)]
+        subs.append(("enc", code.encodeBulkAsync(data, checksums=bool(i % 2)), data, i % 2))
+        erased, ntr, tr, reads, ref_reads = _host_pattern_reads(fam, k, p, s, host[i], rnd)
+        subs.append(("dec", code.decodeBulkAsync(reads, erased, tr, ntr), (erased, ntr, tr, ref_reads), 0))
+    rows = 0
+    for kind, ticket, arg, ck in reversed(subs):
+        if kind == "enc":
+            outs = [np.full(L, 0xA5, np.uint8) for _ in range(p)]
+            crcs = code.collect(ticket, outs)
+            ref = _ref_encode(fam, k, p, s, arg)
+            assert all((a == b).all() for a, b in zip(outs, ref))
+            if ck:
+                assert crcs == [zlib.crc32(r.tobytes()) for r in list(arg) + list(ref)]
+            rows += p
+        else:
+            erased, ntr, tr, ref_reads = arg
+            outs = [np.full(L, 0x5A, np.uint8) for _ in erased]
+            code.collect(ticket, outs)
+            want = _ref_decode(fam, k, p, s, ref_reads, erased, ntr, tr)
+            assert all((a == b).all() for a, b in zip(outs, want))
+            rows += len(erased)
+    assert code.pending() == 0
+    return rows
+
+
+def _check_hbatch(fam, k, p, s, host, rnd):
+    """Host-memory batches (hrs_encode_batch_host, hrs_decode_batch_host):
+    parity in place, then a per-stripe random pattern repaired from host
+    memory, survivors only over PCIe."""
+    n, S, L = k + p, host.shape[0], host.shape[2]
+    code = _code(fam, k, p, s)
+    st = host.copy()
+    st[:, :p] = 0xA5
+    device.encode_batch_host(code, st)
+    for i in range(S):
+        ref = _ref_encode(fam, k, p, s, [host[i, p + c] for c in range(k)])
+        assert all((st[i, r] == ref[r]).all() for r in range(p)), i
+    pats = []
+    for _ in range(S):
+        pat = None
+        while pat is None:
+            pat = _pattern(fam, k, p, s, rnd, allow_empty=True)
+        pats.append(pat)
+    E = max(1, max(len(pt[0]) for pt in pats))
+    er = np.full((S, E), -1, dtype=np.int32)
+    for i, pt in enumerate(pats):
+        er[i, :len(pt[0])] = pt[0]
+    src = host.copy()  # non-codeword rows: every coefficient counts
+    out = np.full((S, E, L), 0x5A, np.uint8)
+    device.decode_batch_host(code, src, er, out)
+    rows = S * p
+    for i, (erased, ntr, tr) in enumerate(pats):
+        if not erased:
+            continue
+        reads = [None if x in ntr else src[i, x] for x in range(n)]
+        if fam == "rs":
+            reads = [np.zeros_like(src[i, 0]) if r is None else r for r in reads]
+        want = _ref_decode(fam, k, p, s, reads, erased, ntr, tr)
+        assert all((out[i, j] == want[j]).all() for j in range(len(erased))), (i, erased)
+        rows += len(erased)
+    return rows
+
+
 def test_differential_fuzz(cuda):
     torch = cuda
     rnd = random.Random(SEED)
@@ -242,6 +352,12 @@ def test_differential_fuzz(cuda):
                 got = _check_batch(torch, fam, k, p, s, st, host, rnd)
             elif entry == "host":
                 got = _check_host(fam, k, p, s, host, rnd)
+            elif entry == "hcrc":
+                got = _check_hcrc(fam, k, p, s, host, rnd)
+            elif entry == "async":
+                got = _check_async(fam, k, p, s, host, rnd)
+            elif entry == "hbatch":
+                got = _check_hbatch(fam, k, p, s, host, rnd)
             else:
                 got = _check_crc(torch, fam, k, p, s, st, host)
             rows[(fam, entry)] += got
