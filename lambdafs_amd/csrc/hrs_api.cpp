@@ -1678,7 +1678,7 @@ hrs_status build_batch_plans(hrs_codec* c, const int* erased, int max_erased, si
       }
     }
     pl.nout = ne;
-    if (pl.nin > hrs::kBatchMaxIn || (ne > 5 && pl.nin > hrs::kMaxInRuntimeWide)) ps.fused = false;
+    if (pl.nin > hrs::kBatchMaxIn) ps.fused = false;
     ps.max_nout = std::max(ps.max_nout, ne);
     ps.max_nin = std::max(ps.max_nin, pl.nin);
     const int id = static_cast<int>(ps.plans.size());
@@ -1687,9 +1687,8 @@ hrs_status build_batch_plans(hrs_codec* c, const int* erased, int max_erased, si
     ps.mats.push_back(std::move(m));
     ps.pat[s] = id;
   }
-  // one launch covers every pattern at (max_nout, max_nin): a wide pattern
-  // (6-8 outputs) and a many-input one (> 8 inputs) cannot share it
-  if (ps.max_nout > 5 && ps.max_nin > hrs::kMaxInRuntimeWide) ps.fused = false;
+  // one launch covers every pattern at (max_nout, max_nin); shapes beyond the
+  // register-resident batch kernel take its streaming form (hrs_batch.hip)
   return HRS_OK;
 }
 

@@ -94,6 +94,93 @@ __global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const Ba
   }
 }
 
+// Streaming form for plans beyond the register-resident shapes (> 16 inputs,
+// or > 8 with 6-8 outputs; wide codes): the stripe's inputs are walked in
+// groups of D rows over two register sets, the next group loading while the
+// current one is sliced and accumulated (as bitsliced_stream_kernel), each
+// group's locations and coefficient words read from the plan by scalar loads.
+template <int NOUT, int D>
+__device__ __forceinline__ void batch_load_group(const ConstPlanPtr pl, int r0, int nin, const uint8_t* sb,
+                                                 uint64_t row_stride, int lane, uint32_t (&rows)[D][8]) {
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (r0 + j < nin) load_row(sb + static_cast<uint64_t>(pl->loc[r0 + j]) * row_stride, lane, rows[j]);
+}
+
+template <int NOUT, int D>
+__device__ __forceinline__ void batch_acc_group(const ConstPlanPtr pl, int r0, int nin, uint32_t (&acc)[NOUT][8],
+                                                uint32_t (&rows)[D][8]) {
+  constexpr int kNinb = NOUT >= 4 ? 16 : 8;  // BitLoop: rolled bit loop from 4 outputs
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    if (r0 + j < nin) {
+      bitslice(rows[j]);
+      const uint64_t w = pl->cw[r0 + j];
+      uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
+      asm volatile("" : "+s"(cw[0]));
+      if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));
+      if constexpr (BitLoop<NOUT, kNinb>::kRolled) {
+#pragma unroll 1
+        for (int b = 0; b < 8; ++b) {
+          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
+          xtime(rows[j]);
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
+          if (b < 7) xtime(rows[j]);
+        }
+      }
+    }
+  }
+}
+
+template <int NOUT, int D>
+__global__ void __launch_bounds__(kBlockThreads) batch_stream_kernel(const BatchArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const ConstPlanPtr plans = (ConstPlanPtr)a.plans;
+  int patv = 0;
+  uint32_t k = 0;
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves, ++k) {
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    if ((k & 63u) == 0) {  // pattern indices of the next 64 tasks, one vector load
+      const uint64_t tl = t + static_cast<uint64_t>(lane) * nwaves;
+      patv = tl < a.ntasks ? a.pat[tl / a.nwin] : 0;
+    }
+    const ConstPlanPtr pl = plans + __builtin_amdgcn_readlane(patv, static_cast<int>(k & 63u));
+    int nin = pl->nin;
+    asm volatile("" : "+s"(nin));
+    const int nout = pl->nout;
+    const uint8_t* sb = a.base + stripe * a.stripe_stride + off;
+    uint32_t acc[NOUT][8];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+    uint32_t ra[D][8], rb[D][8];
+    batch_load_group<NOUT, D>(pl, 0, nin, sb, a.row_stride, lane, ra);
+#pragma unroll 1
+    for (int r0 = 0; r0 < nin; r0 += 2 * D) {
+      if (r0 + D < nin) batch_load_group<NOUT, D>(pl, r0 + D, nin, sb, a.row_stride, lane, rb);
+      batch_acc_group<NOUT, D>(pl, r0, nin, acc, ra);
+      if (r0 + D >= nin) break;
+      if (r0 + 2 * D < nin) batch_load_group<NOUT, D>(pl, r0 + 2 * D, nin, sb, a.row_stride, lane, ra);
+      batch_acc_group<NOUT, D>(pl, r0 + D, nin, acc, rb);
+    }
+    uint8_t* ob = a.out + stripe * a.out_stripe_stride + off;
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      if (o < nout) {
+        bitslice(acc[o]);
+        store_row(ob + static_cast<uint64_t>(o) * a.out_row_stride, lane, acc[o]);
+      }
+    }
+  }
+}
+
 // Byte columns [col0, len) of every stripe (tails, unaligned batches).
 __global__ void __launch_bounds__(kBlockThreads) batch_bytewise_kernel(const BatchArgs a) {
   __shared__ uint8_t s_exp[512];
@@ -148,12 +235,22 @@ hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
 }
 
 template <int NOUT>
+hipError_t launch_batch_stream_n(const BatchArgs& a, hipStream_t s) {
+  auto kern = batch_stream_kernel<NOUT, 4>;
+  const int per_cu = NOUT >= 4 ? 3 : 2;
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NOUT>
 hipError_t launch_batch_nout(const BatchArgs& a, int max_nin, hipStream_t s) {
+  if (max_nin > kBatchMaxIn) return hipErrorInvalidValue;
+  if (max_nin > 16 || (NOUT > 5 && max_nin > 8)) return launch_batch_stream_n<NOUT>(a, s);
   if (max_nin <= 4) return launch_batch_n<NOUT, 4>(a, s);
   if (max_nin <= 8) return launch_batch_n<NOUT, 8>(a, s);
   if constexpr (NOUT < 6) {
     if (max_nin <= 12) return launch_batch_n<NOUT, 12>(a, s);
-    if (max_nin <= 16) return launch_batch_n<NOUT, 16>(a, s);
+    return launch_batch_n<NOUT, 16>(a, s);
   }
   return hipErrorInvalidValue;
 }

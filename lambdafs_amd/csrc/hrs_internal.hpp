@@ -61,7 +61,7 @@ int device_cu_count();  // CUs of the current device (cached)
 
 // ---- heterogeneous batches: one erasure pattern per stripe (hrs_decode_batch_dev)
 
-constexpr int kBatchMaxIn = 16;
+constexpr int kBatchMaxIn = 32;  // > 16 inputs (or > 8 with 6-8 outputs): batch_stream_kernel
 constexpr int kHostBatchSlots = 3;  // chunk slots of the host-memory batch pipeline
 constexpr int kAsyncSlots = 4;      // operations in flight per handle (hrs_*_submit / hrs_collect)
 struct BatchPlan {            // one erasure pattern, a device table entry

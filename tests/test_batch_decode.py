@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 from lambdafs_amd import HipNativeReedSolomonCode, HipReedSolomonCode, HipXORCode, TooManyErasedLocations, device
+from oracle import rs_oracle as C
 
 pytestmark = pytest.mark.gpu
 
@@ -169,3 +170,32 @@ def test_batch_back_to_back_calls_reuse_slots(cuda):
             lost = [int(x) for x in er[s] if x >= 0]
             if lost:
                 assert torch.equal(out[s, :len(lost)], st[s, lost])
+
+
+def test_wide_batches_stream_vs_oracle(cuda):
+    """Patterns beyond the register-resident batch kernel (> 16 survivors, or
+    > 8 with 6-8 outputs) take batch_stream_kernel in one launch; beyond 32
+    survivors, one launch per stripe. Non-codeword rows: every coefficient
+    of every pattern's matrix is checked against the oracle's decodeBulk."""
+    torch = cuda
+    rnd = np.random.default_rng(77)
+    for k, p, S, L in [(20, 8, 12, 4096 + 48), (12, 6, 10, 2048), (40, 4, 3, 2048 + 16)]:
+        n = k + p
+        code = HipReedSolomonCode(k, p)
+        st = _stripes(torch, S, n, L, 80 + k)
+        er = np.full((S, p), -1, dtype=np.int32)
+        for s in range(S):
+            e = sorted(rnd.choice(n, size=int(rnd.integers(0, p + 1)), replace=False).tolist())
+            er[s, :len(e)] = e
+        out = torch.full((S, p, L), 0x5A, dtype=torch.uint8, device="cuda")
+        device.decode_batch(code, st, er, out)
+        host, got = st.cpu().numpy(), out.cpu().numpy()
+        for s in range(S):
+            lost = [int(x) for x in er[s] if x >= 0]
+            if not lost:
+                continue
+            tr = sorted(C.locations_to_read(k, p, lost))
+            ntr = [x for x in range(n) if x not in tr]
+            reads = [host[s, x] if x in tr else np.zeros(L, np.uint8) for x in range(n)]
+            ref = C.decode_bulk5(k, p, reads, lost, tr, ntr)
+            assert all((got[s, j] == ref[j]).all() for j in range(len(lost))), (k, p, s, lost)
