@@ -124,7 +124,7 @@ def test_xor_batch(cuda):
             assert torch.equal(out[s, 0], st[s, int(er[s, 0])])
 
 
-def test_wide_code_batch_falls_back_per_stripe(cuda):
+def test_wide_code_batch_round_trip(cuda):
     torch = cuda
     k, p, S, L = 30, 6, 6, 2048 + 9
     n = k + p
