@@ -62,26 +62,7 @@ __global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const Ba
       for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
 #pragma unroll
     for (int r = 0; r < NINB; ++r) {
-      if (r < nin) {
-        bitslice(rows[r]);
-        const uint64_t w = pl->cw[r];
-        uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
-        asm volatile("" : "+s"(cw[0]));
-        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
-        if constexpr (BitLoop<NOUT, NINB>::kRolled) {
-#pragma unroll 1
-          for (int b = 0; b < 8; ++b) {
-            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
-            xtime(rows[r]);
-          }
-        } else {
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
-            if (b < 7) xtime(rows[r]);
-          }
-        }
-      }
+      if (r < nin) accumulate_row<NOUT, NINB>(acc, rows[r], pl->cw[r]);
     }
     uint8_t* ob = a.out + stripe * a.out_stripe_stride + off;
 #pragma unroll
@@ -112,28 +93,8 @@ __device__ __forceinline__ void batch_acc_group(const ConstPlanPtr pl, int r0, i
                                                 uint32_t (&rows)[D][8]) {
   constexpr int kNinb = NOUT >= 4 ? 16 : 8;  // BitLoop: rolled bit loop from 4 outputs
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    if (r0 + j < nin) {
-      bitslice(rows[j]);
-      const uint64_t w = pl->cw[r0 + j];
-      uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
-      asm volatile("" : "+s"(cw[0]));
-      if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));
-      if constexpr (BitLoop<NOUT, kNinb>::kRolled) {
-#pragma unroll 1
-        for (int b = 0; b < 8; ++b) {
-          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
-          xtime(rows[j]);
-        }
-      } else {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
-          if (b < 7) xtime(rows[j]);
-        }
-      }
-    }
-  }
+  for (int j = 0; j < D; ++j)
+    if (r0 + j < nin) accumulate_row<NOUT, kNinb>(acc, rows[j], pl->cw[r0 + j]);
 }
 
 template <int NOUT, int D>

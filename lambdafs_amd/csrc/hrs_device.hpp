@@ -350,4 +350,31 @@ __device__ __forceinline__ void mul_acc_row(uint32_t (&acc)[NOUT][8], uint32_t (
     }
 }
 
+// acc[o] ^= coef[o] * x for one input row of a window: bit-slice the row,
+// then for every set bit b of each output's coefficient XOR alpha^b x into it
+// (wave-uniform branches). w packs the coefficients (byte o = output o); the
+// empty asm keeps the per-(o, b) tests next to their use instead of hoisted
+// out of the task loop (they would spill). Rolled bit loop when the unrolled
+// body would outgrow the instruction cache (BitLoop). x is consumed.
+template <int NOUT, int NINB>
+__device__ __forceinline__ void accumulate_row(uint32_t (&acc)[NOUT][8], uint32_t (&x)[8], uint64_t w) {
+  bitslice(x);
+  uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
+  asm volatile("" : "+s"(cw[0]));
+  if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
+  if constexpr (BitLoop<NOUT, NINB>::kRolled) {
+#pragma unroll 1
+    for (int b = 0; b < 8; ++b) {
+      mul_acc_row<NOUT, NINB>(acc, x, cw, b);
+      xtime(x);
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      mul_acc_row<NOUT, NINB>(acc, x, cw, b);
+      if (b < 7) xtime(x);
+    }
+  }
+}
+
 }  // namespace hrs

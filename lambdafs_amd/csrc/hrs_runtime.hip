@@ -2,7 +2,7 @@
 // compile-time kernel) as out = M * in with the coefficients of M in the
 // kernel arguments — bit-sliced rows, planes multiplied by alpha and
 // accumulated under wave-uniform branches (see hrs_kernels.hip's header for
-// the arithmetic; bitslice / xtime / mul_acc_row in hrs_device.hpp).
+// the arithmetic; bitslice / xtime / accumulate_row in hrs_device.hpp).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -42,29 +42,7 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
     }
 #pragma unroll
     for (int r = 0; r < NINB; ++r) {
-      if (r < nin) {
-        bitslice(rows[r]);
-        // one wave-uniform 64-bit word per input (byte o = coefficient of
-        // output o), split in halves; the empty asm keeps the per-(o, b)
-        // tests from being hoisted out of the task loop (they would spill).
-        uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
-        asm volatile("" : "+s"(cw[0]));
-        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
-        // acc[o] ^= sum over set bits b of coef[o][r]: alpha^b * row
-        if constexpr (BitLoop<NOUT, NINB>::kRolled) {
-#pragma unroll 1
-          for (int b = 0; b < 8; ++b) {
-            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
-            xtime(rows[r]);
-          }
-        } else {
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
-            if (b < 7) xtime(rows[r]);
-          }
-        }
-      }
+      if (r < nin) accumulate_row<NOUT, NINB>(acc, rows[r], a.cw[r]);  // acc[o] ^= coef[o][r] * row
     }
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
@@ -110,17 +88,7 @@ __device__ __forceinline__ void apply_task(const RowArgs& a, uint64_t t, int nin
   }
 #pragma unroll
   for (int r = 0; r < NINB; ++r) {
-    if (r < nin) {
-      bitslice(rows[r]);
-      uint32_t cw[2] = {static_cast<uint32_t>(a.cw[r]), static_cast<uint32_t>(a.cw[r] >> 32)};
-      asm volatile("" : "+s"(cw[0]));
-        if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));  // outputs 4..7 only
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        mul_acc_row<NOUT, NINB>(acc, rows[r], cw, b);
-        if (b < 7) xtime(rows[r]);
-      }
-    }
+    if (r < nin) accumulate_row<NOUT, NINB>(acc, rows[r], a.cw[r]);
   }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
@@ -176,28 +144,8 @@ __device__ __forceinline__ void acc_group(const RowArgs& a, int r0, int nin, uin
                                           uint32_t (&rows)[D][8]) {
   constexpr int kNinb = NOUT >= 4 ? 16 : 8;  // BitLoop: rolled bit loop from 4 outputs
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    if (r0 + j < nin) {
-      bitslice(rows[j]);
-      const uint64_t w = a.cw[r0 + j];
-      uint32_t cw[2] = {static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)};
-      asm volatile("" : "+s"(cw[0]));
-      if constexpr (NOUT > 4) asm volatile("" : "+s"(cw[1]));
-      if constexpr (BitLoop<NOUT, kNinb>::kRolled) {
-#pragma unroll 1
-        for (int b = 0; b < 8; ++b) {
-          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
-          xtime(rows[j]);
-        }
-      } else {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          mul_acc_row<NOUT, kNinb>(acc, rows[j], cw, b);
-          if (b < 7) xtime(rows[j]);
-        }
-      }
-    }
-  }
+  for (int j = 0; j < D; ++j)
+    if (r0 + j < nin) accumulate_row<NOUT, kNinb>(acc, rows[j], a.cw[r0 + j]);
 }
 
 template <int NOUT, int D>
