@@ -9,14 +9,20 @@ CC       ?= gcc
 LIB      := lambdafs_amd/libhrs.so
 ORACLE   := oracle/liboracle.so
 HDRS     := Makefile include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/hrs_launch.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
-            lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp lambdafs_amd/csrc/xor_sched.hpp
+            lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp lambdafs_amd/csrc/xor_sched.hpp lambdafs_amd/csrc/hrs_codec.hpp \
+            lambdafs_amd/csrc/hrs_host.hpp
+
+# Host translation units of the C ABI (no kernels): lifecycle + queries,
+# matrices, device dispatch + CRC, host-buffer path, batches.
+API_SRC  := hrs_api hrs_matrix hrs_dispatch hrs_hostpath hrs_batch_api
+API_OBJ  := $(patsubst %,build/%.o,$(API_SRC))
 
 JNI      := lambdafs_amd/libhrs_jni.so
-HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic
+HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables
 
 all: $(LIB) $(ORACLE) $(JNI) $(HARNESS)
 
-build/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS)
+$(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
@@ -43,10 +49,14 @@ build/hrs_fused.o: lambdafs_amd/csrc/hrs_fused.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -mllvm -pragma-unroll-threshold=1000000 -c $< -o $@
 
-KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o
+build/hrs_probe.o: lambdafs_amd/csrc/hrs_probe.hip include/hrs_probe.h $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): build/hrs_api.o $(KOBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_probe.o
+
+$(LIB): $(API_OBJ) $(KOBJ) lambdafs_amd/csrc/libhrs.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs.map -o $@ $(API_OBJ) $(KOBJ)
 
 $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/rs_oracle.c
@@ -64,13 +74,18 @@ $(JNI): lambdafs_amd/jni/hrs_jni.c lambdafs_amd/jni/jni_min.h include/hrs.h $(LI
 
 # Fake-JVM harness driving every HrsNative entry point (tests/test_jni.py).
 tests/cpp/jni_harness: tests/cpp/jni_harness.c lambdafs_amd/jni/jni_min.h $(JNI) $(ORACLE)
-	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs_jni -lhrs -Loracle -loracle -lz \
+	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs_jni -lhrs -Loracle -loracle -lz -ldl \
 	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # Host-only logic (matrices, survivor lists, decode cache, batch plans) vs the oracle.
 tests/cpp/host_logic: tests/cpp/host_logic.cpp include/hrs.h $(LIB) $(ORACLE)
 	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ $< -Llambdafs_amd -lhrs -Loracle -loracle \
 	    -Wl,-rpath,'$$ORIGIN/../../lambdafs_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# The CRC tables the kernels load, dumped for tests/test_crc_tables.py (host code;
+# hipcc only for the HIP headers hrs_crc.hpp includes).
+tests/cpp/crc_tables: tests/cpp/crc_tables.cpp lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
+	$(HIPCC) -O2 -std=c++17 -x hip --offload-arch=$(ARCH) -o $@ $<
 
 tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
 	g++ -O2 -std=c++17 -Wall -o $@ $< -lz
@@ -88,11 +103,12 @@ HSAN     := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xar
 ASAN_BIN := $(ASAN_DIR)/host_logic $(ASAN_DIR)/jni_harness $(ASAN_DIR)/codec_harness
 ASAN_LOG := profiles/r02/asan
 
-$(ASAN_DIR)/hrs_api.o: lambdafs_amd/csrc/hrs_api.cpp $(HDRS) lambdafs_amd/csrc/hrs_host.hpp
+ASAN_API := $(patsubst %,$(ASAN_DIR)/%.o,$(API_SRC))
+$(ASAN_API): $(ASAN_DIR)/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p $(ASAN_DIR)
 	$(HIPCC) -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) $(HSAN) -x hip -c $< -o $@
 
-$(ASAN_DIR)/libhrs.so: $(ASAN_DIR)/hrs_api.o $(KOBJ)
+$(ASAN_DIR)/libhrs.so: $(ASAN_API) $(KOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -fsanitize=address,undefined -o $@ $^
 
 $(ASAN_DIR)/liboracle.so: oracle/rs_oracle.c oracle/rs_oracle.h
@@ -107,7 +123,7 @@ $(ASAN_DIR)/host_logic: tests/cpp/host_logic.cpp $(ASAN_DIR)/libhrs.so $(ASAN_DI
 	$(CLANG)++ $(SAN) -std=c++17 -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs -loracle $(ASAN_RPATH)
 
 $(ASAN_DIR)/jni_harness: tests/cpp/jni_harness.c $(ASAN_DIR)/libhrs_jni.so $(ASAN_DIR)/liboracle.so
-	$(CLANG) $(SAN) -std=c11 -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs_jni -lhrs -loracle -lz $(ASAN_RPATH)
+	$(CLANG) $(SAN) -std=c11 -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs_jni -lhrs -loracle -lz -ldl $(ASAN_RPATH)
 
 $(ASAN_DIR)/codec_harness: tests/cpp/codec_harness.cpp include/hrs.hpp $(ASAN_DIR)/libhrs.so $(ASAN_DIR)/liboracle.so
 	$(CLANG)++ $(SAN) -std=c++17 -pthread -Iinclude -Ioracle -o $@ $< -L$(ASAN_DIR) -lhrs -loracle -lz $(ASAN_RPATH)

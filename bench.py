@@ -14,11 +14,23 @@ value = user-data bytes (k * L per stripe, counted once for the encode and
 once for the decode) of all ranks / max-over-ranks wall time, in GiB/s.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
-     (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+     --gpus N > 1 without a launcher: bench.py starts
+         python -m torch.distributed.run --nproc-per-node N bench.py ...
+     as a child process before anything touches the GPU, relays its output and
+     exits with its status (the driver's `python -m torch.distributed.run ...
+     bench.py --gpus N` form runs the ranks directly). A launcher whose
+     WORLD_SIZE differs from --gpus is an error.
+
+After timing, the parity and the decoded rows are hashed per block of 256
+global stripes and compared with the C oracle's digests of the same synthetic
+stripes (tests/golden/bench_digests.json); a mismatch fails the run.
 """
 import argparse
 import json
 import os
+import re
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,16 +40,17 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-import synth  # noqa: E402  (SURVEY §8(d) synthetic stripes: splitmix64 per global stripe)
-from lambdafs_amd import HipReedSolomonCode, device, parallel  # noqa: E402
+
+# Product imports happen in main(), after the launch decision (launch_plan):
+# a relaunching parent must not touch the GPU before it starts its child.
+synth = HipReedSolomonCode = device = parallel = None
 
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -56,7 +69,32 @@ def parse():
     ap.add_argument("--check", action="store_true", help="verify a sample against the oracle after timing")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
-    return ap.parse_args()
+    ap.add_argument("--print-launch", action="store_true",
+                    help="print the launch decision as JSON and exit (no GPU work; tests)")
+    return ap.parse_args(argv)
+
+
+def launch_plan(args, env):
+    """What this process does, decided from --gpus and the launcher's
+    environment alone (no GPU call): "run" the rank(s) here, "spawn" a
+    torch.distributed.run child with --gpus ranks, or refuse a mismatch."""
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        return ("spawn", None) if args.gpus > 1 else ("run", None)
+    if int(world) != args.gpus:
+        return "error", f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks"
+    return "run", None
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_command(args, argv):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
 
 
 def setup_dist(args):
@@ -146,15 +184,19 @@ def cpu_baseline(k, p, L, nstripes, threads=None):
     }
 
 
-def e2e_config5(local, rank, world, S=512, L=256 << 10, reps=3):
+def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     """BASELINE configs[4] end to end through the product's host batch API
     (hrs_decode_batch_host): RS(12,4), 256 KiB cells, S stripes per GPU (4,096
     over 8), a seeded random PAIR of lost locations per stripe (keyed by the
     global stripe index), the stripes in pinned host memory; only each
     stripe's 12 survivors cross PCIe H2D, only the 2 repaired cells come back.
     Also the same path staged from pageable memory, and the host batch encode
-    (hrs_encode_batch_host: 12 data cells H2D, 4 parity cells D2H)."""
-    import torch
+    (hrs_encode_batch_host: 12 data cells H2D, 4 parity cells D2H). The
+    repaired cells are hashed per 256-stripe block and compared with the
+    oracle's digests (golden["config5"]).
+    Host memory per rank: ~2.3 GiB pinned (stripes + repaired cells) and
+    ~4.3 GiB pageable at peak (the pageable copy, its outputs, one D2H check
+    copy): ~6.5 GiB per rank, ~52 GiB on an 8-GPU node."""
     k, p = 12, 4
     n = k + p
     code = HipReedSolomonCode(k, p, device=local)
@@ -188,11 +230,13 @@ def e2e_config5(local, rank, world, S=512, L=256 << 10, reps=3):
     dec_ms = timed(lambda: device.decode_batch_host(code, stn, er, outn))
     idx = np.arange(S)[:, None]
     dec_ok = bool(np.array_equal(outn, stn[idx, er]))
+    mine = block_sha256(lambda a, b: outn[a:b], S, g0)
     # pageable host memory: the same call stages through pinned slots
     pg = np.array(stn)
     pout = np.zeros((S, 2, L), np.uint8)
     pg_ms = timed(lambda: device.decode_batch_host(code, pg, er, pout))
     pg_ok = bool(np.array_equal(pout, pg[idx, er]))
+    del pg, pout
     # the link's own rate for the same survivor bytes: one pinned H2D copy
     nbytes = k * L * S
     src = st.view(-1)[:nbytes]
@@ -204,6 +248,7 @@ def e2e_config5(local, rank, world, S=512, L=256 << 10, reps=3):
     t_enc = parallel.max_over_ranks(float(np.median(enc_ms)), dev)
     t_pg = parallel.max_over_ranks(float(np.median(pg_ms)), dev)
     ok = parallel.all_ok(enc_ok and dec_ok and pg_ok, dev)
+    repaired = gather_blocks(mine, world)
     user = k * L * S * world
 
     def rate(t_ms, nbytes):
@@ -224,46 +269,92 @@ def e2e_config5(local, rank, world, S=512, L=256 << 10, reps=3):
         "encode_GiBps_user": rate(t_enc, user),
         "encode_pcie_GBps": round((k + p) * L * S * world / 1e9 / (t_enc * 1e-3), 2),
         "bit_exact": ok,
+        "repaired_vs_oracle": compare_blocks({"repaired": repaired}, golden.get("config5", {}), ("repaired",)),
         "n_gpus": world,
     }
 
 
-def parity_sha256(stripes, p, g0, block=256):
-    """SHA-256 of this rank's parity rows (rows 0..p-1, L bytes each, stripe
-    by stripe) over each block of `block` consecutive GLOBAL stripes starting
-    at a multiple of `block`: {first global stripe of the block: digest}.
-    Inputs are keyed by global stripe index, so any N-GPU run covering a
-    block must print the same digest for it as any other run."""
+def block_sha256(rows_of, S, g0, block=256):
+    """SHA-256 per block of `block` consecutive GLOBAL stripes (a block starts
+    at a multiple of `block`) of this rank's stripes g0 .. g0+S-1; rows_of(a, b)
+    returns the bytes to hash for local stripes [a, b) (a tensor, device or
+    host, or an array), hashed stripe by stripe in order. {block key: digest},
+    key "g" for a whole block, "g+n" for a partial one. Inputs are keyed by
+    global stripe index, so any N-GPU run covering a block prints the same
+    digest for it, and tests/golden/bench_digests.json holds the oracle's."""
     import hashlib
-    S = stripes.shape[0]
     out = {}
     s = 0
     while s < S:
         g = g0 + s
-        n = min(block - g % block, S - s)
+        nb = min(block - g % block, S - s)
         h = hashlib.sha256()
-        for s0 in range(s, s + n, 64):
-            h.update(stripes[s0:min(s + n, s0 + 64), :p].contiguous().cpu().numpy().tobytes())
-        key = f"{g}" if n == block else f"{g}+{n}"
-        out[key] = h.hexdigest()
-        s += n
+        for s0 in range(s, s + nb, 64):
+            x = rows_of(s0, min(s + nb, s0 + 64))
+            if isinstance(x, torch.Tensor):
+                x = x.contiguous().cpu().numpy()
+            h.update(np.ascontiguousarray(x).tobytes())
+        out[f"{g}" if nb == block else f"{g}+{nb}"] = h.hexdigest()
+        s += nb
     return out
 
 
-def copy_peak(dev, code, nbytes=4 << 30, reps=5):
-    """Measured device-copy (STREAM-copy) rate on this GPU, read + write of a
-    4 GiB buffer, median of `reps`, two ways: the runtime's D2D copy (torch
-    copy_) and the engine's own streaming copy (a 1 x 1 all-ones apply runs
-    xor_kernel: the same NT loads/stores and grid as the coding kernels, no
-    math). SURVEY §8d asks for the roofline against both 8 TB/s and a
-    measured copy peak; frac_vs_copy uses the faster of the two."""
-    rows = nbytes >> 20
-    src = torch.empty((rows, 1 << 20), dtype=torch.uint8, device=dev)
+def gather_blocks(mine, world):
+    """Union of every rank's block digests (all_gather_object)."""
+    allv = [mine]
+    if world > 1:
+        allv = [None] * world
+        dist.all_gather_object(allv, mine)
+    merged = {}
+    for d in allv:
+        merged.update(d)
+    return dict(sorted(merged.items(), key=lambda kv: int(kv[0].split("+")[0])))
+
+
+def load_golden():
+    path = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def compare_blocks(got, want, fields):
+    """Compares printed block digests with the oracle's. Returns None when no
+    block of this run is in the golden file (another workload shape), else
+    {"blocks": n, "match": True}; raises on any mismatch."""
+    n = 0
+    for f in fields:
+        ref = want.get(f, {})
+        for key, dig in got[f].items():
+            if key not in ref:
+                continue
+            if ref[key] != dig:
+                raise RuntimeError(f"{f} block {key}: digest {dig} != oracle {ref[key]}")
+            n += 1
+    return {"blocks": n, "match": True} if n else None
+
+
+def hbm_probes(dev, nbytes=4 << 30, reps=5):
+    """This GPU's streaming ceilings, measured in this run by the engine's
+    probes (include/hrs_probe.h: nontemporal 16-byte grid-stride kernels,
+    256-thread blocks), median of `reps` over 4 GiB buffers:
+      copy  : read + write of 4 GiB (hrs_probe_copy at 2 and 4 blocks per CU,
+              and torch's D2D copy_) — SURVEY §8d's "device-copy STREAM peak";
+      read  : read-only stream (hrs_probe_read, 4 blocks per CU);
+      write : write-only stream (hrs_probe_write, 4 blocks per CU).
+    A 1:1 copy is not a ceiling for the codec's read-heavy mixes (10 reads per
+    4 writes for RS(10,4) encode, per 1 write for a repair): reads and writes
+    share HBM's data bus, so the ceiling of a mix of R bytes read and W
+    written is (R + W) / (R / read + W / write) (mix_ceiling)."""
+    src = torch.empty((nbytes >> 20, 1 << 20), dtype=torch.uint8, device=dev)
     src.fill_(0x5A)
     dst = torch.empty_like(src)
+    sink = torch.zeros(4096, dtype=torch.uint8, device=dev)
     out = {}
-    for name, fn in (("torch_copy", lambda: dst.copy_(src)),
-                     ("engine_copy", lambda: device.apply_rows(code, [[1]], [src], [dst]))):
+
+    def timed(fn):
         fn()
         times = []
         for _ in range(reps):
@@ -273,14 +364,36 @@ def copy_peak(dev, code, nbytes=4 << 30, reps=5):
             b.record()
             b.synchronize()
             times.append(a.elapsed_time(b))
-        out[name] = round(2 * nbytes / (float(np.median(times)) * 1e-3) / 1e9, 1)
-    if not torch.equal(dst[::97], src[::97]):
-        raise RuntimeError("copy probe mismatch")
-    del src, dst
+        return float(np.median(times))
+
+    for name, fn in (("probe_nt_4cu", lambda: device.probe_copy(src, dst, 4)),
+                     ("probe_nt_2cu", lambda: device.probe_copy(src, dst, 2)),
+                     ("torch_copy", lambda: dst.copy_(src))):
+        out[name] = round(2 * nbytes / (timed(fn) * 1e-3) / 1e9, 1)
+        if not torch.equal(dst[::97], src[::97]):
+            raise RuntimeError(f"copy probe {name} mismatch")
+        dst.zero_()
+    read = round(nbytes / (timed(lambda: device.probe_read(src, sink, 4)) * 1e-3) / 1e9, 1)
+    write = round(nbytes / (timed(lambda: device.probe_write(dst, 4)) * 1e-3) / 1e9, 1)
+    if int(sink.sum().item()) != 0 or dst[0, 4:8].tolist() != [0x5A] * 4:  # element 0 = (0, 0x5A5A5A5A, ..)
+        raise RuntimeError("read / write probes did not run as intended")
+    del src, dst, sink
     torch.cuda.empty_cache()
-    out["GBps"] = max(out["torch_copy"], out["engine_copy"])
-    out["how"] = "4 GiB D2D, median of 5: torch copy_ and the engine's 1x1 streaming copy; GBps = max"
-    return out
+    copy = max(out["probe_nt_4cu"], out["probe_nt_2cu"], out["torch_copy"])
+    return {
+        "copy": {**out, "GBps": copy,
+                 "how": "4 GiB D2D, median of 5: hrs_probe_copy (nontemporal float4 grid-stride copy, 256-thread "
+                        "blocks, 2 and 4 per CU) and torch copy_; GBps = the fastest"},
+        "read_GBps": read,
+        "write_GBps": write,
+        "how": "hrs_probe_read / hrs_probe_write over 4 GiB, 4 blocks per CU, median of 5",
+    }
+
+
+def mix_ceiling(probes, rbytes, wbytes):
+    """Ceiling of a stream of rbytes read and wbytes written on this GPU:
+    reads and writes share the HBM data bus, each at its own measured peak."""
+    return (rbytes + wbytes) / (rbytes / probes["read_GBps"] + wbytes / probes["write_GBps"])
 
 
 def stats(ms):
@@ -288,32 +401,52 @@ def stats(ms):
             "min": round(float(np.min(ms)), 4)}
 
 
-# The software-pipelined kernels are the default (HRS_PIPE=0: the plain ones);
-# names as rocprofv3 reports them, keys of profiles/pmc_traffic.json.
-PIPE = os.environ.get("HRS_PIPE", "1") != "0"
-DEC_KERNEL = "bitsliced_pipe_kernel<1,12>" if PIPE else "bitsliced_kernel<1,12>"
-BATCH_KERNEL = ("batch_bitsliced_kernel<1,12,true>" if os.environ.get("HRS_BATCH_PATV", "1") != "0"
-                else "batch_bitsliced_kernel<1,12,false>")
-
-
-def enc_kernel_name(k, p):
-    return f"encode_static_kernel<{k},{p}>"
+def traffic_key(name):
+    """rocprofv3 kernel name -> the key tools/pmc_traffic.py files it under:
+    the name up to its first '>' without namespace or parameters, ", " -> ","."""
+    name = re.sub(r"^.*::", "", name.split("(")[0]) if "::" in name.split("<")[0] else name
+    m = re.match(r"([A-Za-z_0-9]+(?:<[^>]*>)?)", name)
+    return m.group(1).replace(", ", ",") if m else name
 
 
 def load_traffic(kernel):
+    """PMC HBM bytes per launch of `kernel` (the name the run launched) from
+    profiles/pmc_traffic.json; raises if the kernel has no entry, so a kernel
+    change cannot silently print stale or missing traffic."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f).get(kernel)
-    except (OSError, ValueError):
-        return None
+    with open(path) as f:
+        table = json.load(f)
+    key = traffic_key(kernel)
+    if key not in table:
+        raise RuntimeError(f"no PMC traffic for kernel {key} in {path}: profile it (profiles/run_rocprof.sh)")
+    return table[key]
 
 
 def main():
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    plan, why = launch_plan(args, os.environ)
+    if args.print_launch:
+        print(json.dumps({"plan": plan, "why": why, "cuda_initialized": torch.cuda.is_initialized(),
+                          "command": spawn_command(args, argv) if plan == "spawn" else None}))
+        return 0
+    if plan == "error":
+        print(f"bench.py: {why}", file=sys.stderr)
+        return 2
+    if plan == "spawn":
+        # one rank per GPU, started before this process makes any GPU call
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        return subprocess.call(spawn_command(args, argv), env=env)
+    return run(args)
+
+
+def run(args):
+    global synth, HipReedSolomonCode, device, parallel
+    import synth as _synth  # SURVEY §8(d) synthetic stripes: splitmix64 per global stripe
+    from lambdafs_amd import HipReedSolomonCode as _Code, device as _device, parallel as _parallel
+    synth, HipReedSolomonCode, device, parallel = _synth, _Code, _device, _parallel
+
     world, rank, local = setup_dist(args)
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     k, p, L = args.k, args.p, args.cell
     if args.strong:
         lo, hi = parallel.stripe_range(args.stripes, world, rank)
@@ -323,6 +456,7 @@ def main():
     n = k + p
     dev = f"cuda:{local}"
     code = HipReedSolomonCode(k, p, device=local)
+    golden = load_golden()
 
     # coding matrices: built on rank 0, broadcast over RCCL, checked everywhere
     erased = [p]  # data shard 0 = hops location p
@@ -365,6 +499,10 @@ def main():
     torch.cuda.synchronize()
     parallel.barrier()
     elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
+    dec_kernel = code.lastKernel()  # the decode step's kernel (apply_rows ran last)
+    device.encode_stripes(code, stripes)  # idempotent: same parity; names the encode kernel
+    enc_kernel = code.lastKernel()
+    torch.cuda.synchronize()
 
     enc_all = [e[0].elapsed_time(e[1]) for e in events]
     dec_all = [e[1].elapsed_time(e[2]) for e in events]
@@ -385,13 +523,14 @@ def main():
         raise RuntimeError("benchmark output failed its round-trip check")
 
     # SURVEY §8(d) config 3, second run: a seeded random lost location per
-    # stripe, all repaired in one launch (hrs_decode_batch_dev); reported
-    # beside the headline, outside its timed region
-    rnd = np.random.default_rng(0x5EED0003 + rank)
-    er_rand = rnd.integers(0, n, (S, 1)).astype(np.int32)
+    # stripe (keyed by the global stripe index), all repaired in one launch
+    # (hrs_decode_batch_dev); reported beside the headline, outside its timed region
+    er_rand = np.array([[np.random.default_rng([0x5EED0003, g0 + s]).integers(0, n)] for s in range(S)],
+                       dtype=np.int32)
     out_rand = torch.empty((S, 1, L), dtype=torch.uint8, device=dev)
     device.decode_batch(code, stripes, er_rand, out_rand)
     torch.cuda.synchronize()
+    batch_kernel = code.lastKernel()
     rand_ms = []
     for _ in range(max(3, min(args.steps, 10))):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -424,6 +563,7 @@ def main():
 
     cells = [stripes[:, p + c, :] for c in range(k)] + [stripes[:, r, :] for r in range(p)]
     crc_fused = device.encode_stripes_crc(code, stripes)
+    fused_kernel = code.lastKernel()
     crc_two = device.crc32_rows(code, cells)
     if not parallel.all_ok(bool(torch.equal(crc_fused, crc_two)), dev):
         raise RuntimeError("fused encode+CRC differs from encode then CRC")
@@ -431,21 +571,24 @@ def main():
     fused_ms = med_ms(lambda: device.encode_stripes_crc(code, stripes), reps)
     two_ms = med_ms(lambda: (device.encode_stripes(code, stripes), device.crc32_rows(code, cells)), reps)
 
+    # the timed outputs against the oracle: parity and decoded rows per block
+    # of 256 global stripes vs tests/golden/bench_digests.json
     sha = None
+    vs_oracle = None
     if not args.no_sha:
-        mine = parity_sha256(stripes, p, g0)
-        allv = [mine]
-        if world > 1:
-            allv = [None] * world
-            dist.all_gather_object(allv, mine)
-        sha = {"block_stripes": 256, "blocks": {}}
-        for d in allv:
-            sha["blocks"].update(d)
+        digs = {"parity": gather_blocks(block_sha256(lambda a, b: stripes[a:b, :p], S, g0), world),
+                "decode": gather_blocks(block_sha256(lambda a, b: out[a:b], S, g0), world)}
+        sha = {"block_stripes": 256, "blocks": digs["parity"], "decode_blocks": digs["decode"]}
+        want = golden.get("config3", {})
+        if (k, p, L) == (want.get("k"), want.get("p"), want.get("cell")):
+            vs_oracle = compare_blocks(digs, want, ("parity", "decode"))
     e2e = None
     if not args.no_e2e:
         del cells
         torch.cuda.empty_cache()
-        e2e = e2e_config5(local, rank, world)
+        e2e = e2e_config5(local, rank, world, golden)
+        if e2e["repaired_vs_oracle"] is None:
+            raise RuntimeError("config 5 repaired cells: no oracle digest to compare with")
 
     total_stripes = args.stripes if args.strong else S * world
     user_bytes = 2 * k * L * total_stripes * args.steps
@@ -453,10 +596,11 @@ def main():
     dec_bytes = (k + len(erased)) * L * S
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
-    kernel = enc_kernel_name(k, p)
     res = None
-    peak = copy_peak(dev, code) if rank == 0 else None
+    probes = hbm_probes(dev) if rank == 0 else None
     if rank == 0:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            traffic_note = json.load(f).get("_note")
         res = {
             "metric": "RS encode+decode GiB/s device-resident; 1/2/4/8 MI355X; %HBM roofline",
             "value": round(user_bytes / GiB / elapsed, 3),
@@ -477,47 +621,55 @@ def main():
                 "stripes_per_gpu": S, "stripes_total": total_stripes, "cell_bytes": L, "k": k, "p": p,
                 "parallelism": f"stripe-sharded x{world} (RCCL: matrix broadcast + barriers only)",
             },
+            "parity_vs_oracle": vs_oracle,
             "encode_GiBps_per_gpu": round(k * L * S / GiB / (enc_ms * 1e-3), 3),
             "decode_GiBps_per_gpu": round(k * L * S / GiB / (dec_ms * 1e-3), 3),
             "roofline": {
-                "kernel": kernel,
+                "kernel": traffic_key(enc_kernel),
                 "bound": "hbm",
                 "achieved": round(enc_gbps, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic(kernel),
+                "traffic": load_traffic(enc_kernel),
+                "traffic_source": traffic_note,
                 "avg_launch_ms": round(enc_ms, 4),
                 "launch_ms": stats(enc_all),
                 "algorithmic_bytes_per_launch": enc_bytes,
-                "copy_peak": peak["GBps"],
-                "frac_vs_copy": round(enc_gbps / peak["GBps"], 4),
+                "copy_peak": probes["copy"]["GBps"],
+                "frac_vs_copy": round(enc_gbps / probes["copy"]["GBps"], 4),
+                "mix_ceiling": round(mix_ceiling(probes, k, p), 1),
+                "frac_vs_mix_ceiling": round(enc_gbps / mix_ceiling(probes, k, p), 4),
             },
             "decode_roofline": {
-                "kernel": DEC_KERNEL, "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
+                "kernel": traffic_key(dec_kernel), "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(dec_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(dec_ms, 4),
-                "launch_ms": stats(dec_all), "frac_vs_copy": round(dec_gbps / peak["GBps"], 4),
-                "traffic": load_traffic(DEC_KERNEL),
+                "launch_ms": stats(dec_all), "frac_vs_copy": round(dec_gbps / probes["copy"]["GBps"], 4),
+                "mix_ceiling": round(mix_ceiling(probes, k, len(erased)), 1),
+                "frac_vs_mix_ceiling": round(dec_gbps / mix_ceiling(probes, k, len(erased)), 4),
+                "traffic": load_traffic(dec_kernel),
                 "algorithmic_bytes_per_launch": dec_bytes,
             },
             "random_location_decode": {
-                "what": "config 3 second run: one seeded random lost location per stripe, one batch launch",
+                "what": "config 3 second run: one seeded random lost location per stripe "
+                        "(default_rng([0x5EED0003, global stripe])), one batch launch",
                 "launch_ms": stats(rand_ms),
-                "kernel": BATCH_KERNEL,
+                "kernel": traffic_key(batch_kernel),
                 "GBps_algorithmic": round((k + 1) * L * S / (float(np.median(rand_ms)) * 1e-3) / 1e9, 1),
                 "algorithmic_bytes_per_launch": (k + 1) * L * S,
-                "traffic": load_traffic(BATCH_KERNEL),
+                "traffic": load_traffic(batch_kernel),
                 "GiBps_user_per_gpu": round(k * L * S / GiB / (float(np.median(rand_ms)) * 1e-3), 3),
             },
             "encode_crc": {
                 "what": "encode + java.util.zip.CRC32 of all k+p cells (Encoder with computeBlockChecksum)",
-                "kernel": f"encode_crc_grouped_kernel<{k},{p},G={4 if k >= 12 else 2},factored> + crc_fold_kernel",
+                "kernel": traffic_key(fused_kernel) + " + crc_fold_kernel",
                 "fused_ms": stats(fused_ms),
                 "two_pass_ms": stats(two_ms),
                 "fused_GBps_algorithmic": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9, 1),
+                "fused_frac": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "speedup_vs_two_pass": round(float(np.median(two_ms)) / float(np.median(fused_ms)), 3),
             },
-            "copy_peak": peak,
+            "hbm_probes": probes,
             "parity_sha256": sha,
             "e2e_config5": e2e,
             "cpu_baseline": None,
@@ -530,7 +682,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

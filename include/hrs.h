@@ -103,6 +103,11 @@ hrs_status hrs_src_layout(const hrs_codec* codec, int* src_parities, int* rs_par
 void hrs_destroy(hrs_codec* codec);
 /* Last error message of this handle ("" if none); handle may be NULL for create errors. */
 const char* hrs_last_error(const hrs_codec* codec);
+/* Name of the main kernel the handle's latest coding call launched, as
+ * rocprofv3 prints it without its namespace and parameters (e.g.
+ * "encode_static_kernel<10, 4>"); "" before any device work. Lets a
+ * benchmark attach the PMC traffic of the kernel it actually ran. */
+const char* hrs_last_kernel(const hrs_codec* codec);
 const char* hrs_version(void);
 
 /* ErasureCode.stripeSize()/paritySize()/symbolSize() (ReedSolomonCode.java:213-226). */
@@ -214,6 +219,12 @@ hrs_status hrs_decode_submit(hrs_codec* codec, const uint8_t* const* read_bufs, 
  * num_erased running java.util.zip.CRC32 values (0 = a fresh CRC32), each
  * continued over this operation's cell (CRC32.update chaining). */
 hrs_status hrs_collect(hrs_codec* codec, uint64_t ticket, uint8_t* const* outputs, uint32_t* crc_io);
+/* Waits until the operation's H2D, kernel and D2H have completed, without
+ * copying anything out or releasing it (hrs_collect still must be called;
+ * it then returns without blocking). Lets a binding wait before it pins the
+ * caller's output rows: the JNI shim calls it outside any
+ * GetPrimitiveArrayCritical region. HRS_EINVAL for an unknown ticket. */
+hrs_status hrs_wait(hrs_codec* codec, uint64_t ticket);
 /* Uncollected operations of this handle. */
 int hrs_pending(const hrs_codec* codec);
 /* Shape of an uncollected operation: output rows, their length, CRC values

@@ -181,7 +181,17 @@ class HipCode : public ErasureCode {
     return t;
   }
 
+  // outputs must hold the operation's output rows exactly, and *crcs (a
+  // checksummed operation only) its CRC values: hrs_collect writes that many.
   void collect(uint64_t ticket, const std::vector<uint8_t*>& outputs, std::vector<uint32_t>* crcs) {
+    int nout = 0, ncrc = 0;
+    size_t len = 0;
+    check(hrs_ticket_shape(h_, ticket, &nout, &len, &ncrc), h_);
+    if (static_cast<int>(outputs.size()) != nout)
+      throw std::invalid_argument("collect: " + std::to_string(outputs.size()) + " output rows, the operation has " +
+                                  std::to_string(nout));
+    if (ncrc > 0 && (!crcs || static_cast<int>(crcs->size()) != ncrc))
+      throw std::invalid_argument("collect: the operation keeps " + std::to_string(ncrc) + " CRC values");
     check(hrs_collect(h_, ticket, outputs.data(), crcs ? crcs->data() : nullptr), h_);
   }
 

@@ -27,7 +27,8 @@ HRS_CODE_XOR = 1
 HRS_CODE_NRS = 2
 HRS_CODE_SRC = 3
 
-# Every entry point declared in include/hrs.h (checked by tests/test_abi.py).
+# Every entry point declared in include/hrs.h and include/hrs_probe.h
+# (checked by tests/test_abi.py).
 EXPORTS = (
     "hrs_create", "hrs_create_code", "hrs_create_src", "hrs_src_layout", "hrs_code_kind", "hrs_destroy",
     "hrs_last_error", "hrs_version", "hrs_locations_to_read_list",
@@ -37,7 +38,7 @@ EXPORTS = (
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
     "hrs_encode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
-    "hrs_set_kernel_mode",
+    "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_probe_copy", "hrs_probe_read", "hrs_probe_write", "hrs_wait",
 )
 
 
@@ -102,8 +103,13 @@ def lib():
         "hrs_decode_submit": ([P, PP, IP, I, IP, I, IP, I, S, I, ctypes.POINTER(ctypes.c_uint64)], I),
         "hrs_collect": ([P, ctypes.c_uint64, PP, P], I),
         "hrs_pending": ([P], I),
+        "hrs_wait": ([P, ctypes.c_uint64], I),
         "hrs_ticket_shape": ([P, ctypes.c_uint64, IP, ctypes.POINTER(ctypes.c_size_t), IP], I),
         "hrs_set_kernel_mode": ([P, I], I),
+        "hrs_last_kernel": ([P], ctypes.c_char_p),
+        "hrs_probe_copy": ([P, P, S, I, P], I),
+        "hrs_probe_read": ([P, S, I, P, P], I),
+        "hrs_probe_write": ([P, S, I, P], I),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

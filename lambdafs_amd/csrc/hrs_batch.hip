@@ -190,6 +190,7 @@ bool use_pat_prefetch() {
 template <int NOUT, int NINB>
 hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
   auto kern = use_pat_prefetch() ? batch_bitsliced_kernel<NOUT, NINB, true> : batch_bitsliced_kernel<NOUT, NINB, false>;
+  note_kernel_t("batch_bitsliced_kernel", NOUT, NINB, use_pat_prefetch());
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
@@ -198,6 +199,7 @@ hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
 template <int NOUT>
 hipError_t launch_batch_stream_n(const BatchArgs& a, hipStream_t s) {
   auto kern = batch_stream_kernel<NOUT, 4>;
+  note_kernel_t("batch_stream_kernel", NOUT, 4);
   const int per_cu = NOUT >= 4 ? 3 : 2;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
@@ -234,6 +236,7 @@ hipError_t launch_batch_bitsliced(const BatchArgs& a, int max_nout, int max_nin,
 
 hipError_t launch_batch_bytewise(const BatchArgs& a, hipStream_t s) {
   const unsigned g = grid_for(batch_bytewise_kernel, kBlockThreads, a.ntasks);
+  note_kernel("batch_bytewise_kernel");
   hipLaunchKernelGGL(batch_bytewise_kernel, dim3(g), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }

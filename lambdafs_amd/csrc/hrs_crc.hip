@@ -148,6 +148,7 @@ hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStr
   if (g == 0) g = 1;
   const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
   auto k = aligned ? crc_window_kernel<true> : crc_window_kernel<false>;
+  note_kernel(aligned ? "crc_window_kernel<true>" : "crc_window_kernel<false>");
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;
@@ -161,6 +162,7 @@ hipError_t launch_crc_fold(const CrcFoldArgs& a, int cus, hipStream_t s) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_fold_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm));
   if (e != hipSuccess) return e;
+  note_kernel("crc_fold_kernel");
   hipLaunchKernelGGL(crc_fold_kernel, dim3(g), dim3(256), shm, s, a);
   return hipGetLastError();
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "crc32.hpp"
 
@@ -19,6 +20,24 @@ constexpr int kCrcSliceWords = 4 * 256 * kCrcRep;           // 128 KiB
 constexpr int kCrcLdsWordsA = kCrcSliceWords + 7 * 1024;    // + Z_1024, Z_{16*2^t} t = 0..5 (156 KiB)
 constexpr int kCrcLdsWordsB = 9 * 1024;                     // Z_window, 6 tree levels, Z_tail, Z_len (36 KiB)
 constexpr int kCrcFoldBlocksPerCU = 3;
+
+// The LDS image of the window kernels (crc_window_kernel, the fused encode +
+// CRC), built on the host and uploaded once per handle: the slicing-by-4
+// tables (kCrcRep bank-private copies; table j = a byte followed by j more
+// bytes of its word, i.e. the zlib slicing tables T8_0..T8_3), then Z_chunk
+// (joins a lane's successive pieces, `chunk` bytes apart) and the lane tree
+// Z_{piece * 2^t}, t = 0..5 (lane l + 2^t is piece * 2^t bytes later).
+// tests/cpp/crc_tables dumps it for tests/test_crc_tables.py.
+inline std::vector<uint32_t> crc_window_image(uint64_t piece, uint64_t chunk) {
+  std::vector<uint32_t> h(kCrcLdsWordsA);
+  const crc::Slice4 sl = crc::make_slice4();
+  for (int j = 0; j < 4; ++j)
+    for (int v = 0; v < 256; ++v)
+      for (int r = 0; r < kCrcRep; ++r) h[crc_slice_word(j, v, r)] = sl.s[j].t[v];
+  crc::to_tables(crc::zeros(chunk), &h[kCrcSliceWords]);
+  for (int t = 0; t < 6; ++t) crc::to_tables(crc::zeros(piece << t), &h[kCrcSliceWords + (1 + t) * 1024]);
+  return h;
+}
 
 struct CrcWinArgs {
   const uint8_t* rows[kCrcMaxRows];

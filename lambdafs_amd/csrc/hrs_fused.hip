@@ -21,8 +21,10 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 
 #include "hrs_device.hpp"
+#include "hrs_launch.hpp"
 
 namespace hrs {
 namespace {
@@ -276,19 +278,29 @@ using CrcKernel = void (*)(const EncodeCrcArgs);
 struct CrcPick {
   CrcKernel k;
   int threads;
+  const char* base;  // kernel name (rocprofv3 form: base<K, P, MATRIX, threads, G, sched>)
+  int g;
+  int sched;  // -1: row-serial kernel (no G / SCHED arguments)
 };
+
+template <class MATRIX> constexpr const char* kMatrixName = "";
+template <int K, int P> constexpr const char* kMatrixName<gf::EncodeMatrix<K, P>> = "hrs::gf::EncodeMatrix";
+template <int K, int P> constexpr const char* kMatrixName<gf::CauchyMatrix<K, P>> = "hrs::gf::CauchyMatrix";
 
 template <int K, int P, class MATRIX>
 CrcPick pick_kernel() {
-  if (fused_variant() == 1) return {encode_crc_kernel<K, P, MATRIX, kFusedThreads>, kFusedThreads};
+  constexpr const char* kg = "encode_crc_grouped_kernel";
+  if (fused_variant() == 1) return {encode_crc_kernel<K, P, MATRIX, kFusedThreads>, kFusedThreads, "encode_crc_kernel", 0, -1};
   const int g = fused_group() ? fused_group() : kFusedGroup<K>;
   if (fused_variant() == 3) {  // factored XOR network (xor_sched.hpp has G = 2, min(4, K), K)
-    if (g == 4) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, (K > 4 ? 4 : K), true>, kFusedThreads};
-    return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2, true>, kFusedThreads};
+    if (g == 4)
+      return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, (K > 4 ? 4 : K), true>, kFusedThreads, kg,
+              (K > 4 ? 4 : K), 1};
+    return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2, true>, kFusedThreads, kg, 2, 1};
   }
-  if (g == 4) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 4, false>, kFusedThreads};
-  if (g == 1) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 1, false>, kFusedThreads};
-  return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2, false>, kFusedThreads};
+  if (g == 4) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 4, false>, kFusedThreads, kg, 4, 0};
+  if (g == 1) return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 1, false>, kFusedThreads, kg, 1, 0};
+  return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, 2, false>, kFusedThreads, kg, 2, 0};
 }
 
 template <int K, int P, class MATRIX>
@@ -296,6 +308,11 @@ hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
   const uint64_t ntasks = a.nstripes * a.nwin;
   const CrcPick k = pick_kernel<K, P, MATRIX>();
+  const std::string mat = std::string(kMatrixName<MATRIX>) + "<" + std::to_string(K) + ", " + std::to_string(P) + ">";
+  if (k.sched < 0)
+    note_kernel_t(k.base, K, P, mat.c_str(), k.threads);
+  else
+    note_kernel_t(k.base, K, P, mat.c_str(), k.threads, k.g, k.sched != 0);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k.k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;

@@ -1,0 +1,490 @@
+// Host-buffer calls, the JNI path: synchronous encodeBulk / decodeBulk over
+// pageable rows through two pinned staging slots (with optional block
+// CRC-32s chained on the host), and the asynchronous submit / wait / collect
+// rounds over a ring of operation slots.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hrs.h"
+#include "hrs_codec.hpp"
+#include "crc32.hpp"
+#include "hrs_host.hpp"
+#include "hrs_internal.hpp"
+
+namespace hrs::api {
+
+// Device scratch for the host-buffer calls: `rows` rows of `pitch` bytes.
+size_t pitch_for(size_t len) { return (len + 255) & ~static_cast<size_t>(255); }
+
+// Host rows -> device, apply m, device -> host rows; synchronous. The rows
+// (pageable: a JNI-pinned Java array) go through pinned staging in column
+// chunks over two slots: while the copy pool moves chunk j into one slot's
+// staging (and chunk j-2's outputs out of it), the GPU runs chunk j-1's H2D,
+// kernel and D2H on the other slot's stream.
+size_t host_chunk_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("HRS_HOST_CHUNK");
+    long x = e ? atol(e) : 0;
+    if (x < static_cast<long>(hrs::kWindowBytes)) x = 512 << 10;  // measured best (tools/host_sweep.sh)
+    return static_cast<size_t>(x) / hrs::kWindowBytes * hrs::kWindowBytes;
+  }();
+  return v;
+}
+
+hrs_status host_slot(hrs_codec* c, int i, size_t bytes) {
+  hrs_codec::HostSlot& h = c->host[i];
+  if (!h.stream) {
+    hipError_t e = hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(c, e, "hipStreamCreate");
+    e = hipEventCreateWithFlags(&h.done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+  }
+  if (h.bytes >= bytes) return HRS_OK;
+  (void)hipStreamSynchronize(h.stream);
+  if (h.dev) (void)hipFree(h.dev);
+  if (h.pin) (void)hipHostFree(h.pin);
+  h.dev = nullptr;
+  h.pin = nullptr;
+  h.bytes = 0;
+  hipError_t e = hipMalloc(&h.dev, bytes);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  e = hipHostMalloc(&h.pin, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  h.bytes = bytes;
+  return HRS_OK;
+}
+
+
+// Block checksums carried through a host-buffer call (Encoder.java:408-450,
+// Decoder.java:222-229 / :645-655): kCrcEncode = CRC-32 of the k inputs then
+// the p outputs (the encode matrix is c->g), kCrcOutputs = of the nout outputs.
+// Each chunk's CRCs come back with its outputs and are chained on the host,
+// crc = Z_len(crc) ^ crc_chunk (zlib crc32_combine), starting from `in`
+// (NULL = fresh CRC32 objects).
+enum HostCrcMode { kCrcNone = 0, kCrcEncode = 1, kCrcOutputs = 2 };
+struct HostCrc {
+  int mode = kCrcNone;
+  const uint32_t* in = nullptr;
+  uint32_t* out = nullptr;
+};
+
+const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
+  auto it = c->crc_zmats.find(len);
+  if (it == c->crc_zmats.end()) it = c->crc_zmats.emplace(len, hrs::crc::zeros(len)).first;
+  return it->second;
+}
+
+hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                           uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc) {
+  const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
+  if (ncrc > 0) {  // the running values; an empty call leaves them as they are
+    for (int r = 0; r < ncrc; ++r) crc.out[r] = crc.in ? crc.in[r] : 0u;
+  }
+  if (len == 0 || nout == 0) return HRS_OK;
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  std::vector<int> slot_of(nin, -1);  // staging row of each live input
+  int nlive = 0;
+  for (int i = 0; i < nin; ++i) {
+    bool any = crc.mode == kCrcEncode;  // every source is checksummed
+    for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
+    if (!any) continue;
+    if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
+    slot_of[i] = nlive++;
+  }
+  for (int o = 0; o < nout; ++o)
+    if (!out_rows[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  const size_t chunk = std::min(len, host_chunk_bytes());
+  const size_t pitch = pitch_for(chunk);
+  const size_t nchunks = (len + chunk - 1) / chunk;
+  // slot layout: nlive + nout rows of `pitch`, then (CRC only) the chunk's
+  // ncrc CRC words, then the raw window-CRC scratch (device side only)
+  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
+  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
+  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(chunk, 1, ncrc) : crc_off;
+  for (int i = 0; i < 2; ++i) {
+    hrs_status st = host_slot(c, i, need);
+    if (st != HRS_OK) return st;
+  }
+  hrs::CopyPool& pool = hrs::CopyPool::instance();
+  std::vector<hrs::CopyJob> jobs;
+  size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
+  bool pending[2] = {false, false};
+  auto finish = [&](int sl) -> hrs_status {  // wait for a slot, copy its outputs out
+    if (!pending[sl]) return HRS_OK;
+    hipError_t e = hipEventSynchronize(c->host[sl].done);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
+    jobs.clear();
+    for (int o = 0; o < nout; ++o)
+      jobs.push_back({out_rows[o] + pend_off[sl], c->host[sl].pin + pitch * (nlive + o), pend_len[sl]});
+    pool.run(jobs);
+    if (ncrc) {  // chunks finish in order: chain this one onto the running values
+      const uint32_t* part = reinterpret_cast<const uint32_t*>(c->host[sl].pin + crc_off);
+      const hrs::crc::Mat& z = crc_zmat(c, pend_len[sl]);
+      for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[r];
+    }
+    pending[sl] = false;
+    return HRS_OK;
+  };
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  for (size_t j = 0; j < nchunks; ++j) {
+    const int sl = static_cast<int>(j & 1);
+    hrs_codec::HostSlot& h = c->host[sl];
+    hrs_status st = finish(sl);
+    if (st != HRS_OK) return st;
+    const size_t off = j * chunk, lj = std::min(chunk, len - off);
+    jobs.clear();
+    for (int i = 0; i < nin; ++i)
+      if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
+    pool.run(jobs);
+    if (nlive > 0) {
+      hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
+    }
+    for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? h.dev + pitch * slot_of[i] : nullptr;
+    for (int o = 0; o < nout; ++o) dout[o] = h.dev + pitch * (nlive + o);
+    uint32_t* dcrc = reinterpret_cast<uint32_t*>(h.dev + crc_off);
+    uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
+    if (crc.mode == kCrcEncode)
+      st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+    else
+      st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
+    if (st != HRS_OK) return st;
+    if (crc.mode == kCrcOutputs) {
+      std::vector<size_t> strides(nout, 0);
+      st = run_crc(c, dout.data(), strides.data(), nout, lj, 1, nullptr, dcrc, h.stream, draw);
+      if (st != HRS_OK) return st;
+    }
+    // outputs (and the chunk CRCs right behind them) back to the staging
+    const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + lj;
+    hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost, h.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+    e = hipEventRecord(h.done, h.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+    pending[sl] = true;
+    pend_off[sl] = off;
+    pend_len[sl] = lj;
+  }
+  for (size_t j = nchunks > 2 ? nchunks - 2 : 0; j < nchunks; ++j) {
+    hrs_status st = finish(static_cast<int>(j & 1));
+    if (st != HRS_OK) return st;
+  }
+  return HRS_OK;
+}
+
+// A call that fails part-way may leave a slot's H2D / kernel / D2H in
+// flight; the next call would then memcpy into staging the DMA engine is
+// still reading or writing. So a failed call drains both slot streams before
+// it returns (a successful one has already waited for every slot it used).
+hrs_status host_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                      uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc = HostCrc()) {
+  const hrs_status st = host_apply_impl(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc);
+  if (st != HRS_OK)
+    for (auto& h : c->host)
+      if (h.stream) (void)hipStreamSynchronize(h.stream);
+  return st;
+}
+
+// ---------------------------------------- asynchronous host-buffer calls
+// An Encoder / Decoder round split in two: submit copies the caller's rows
+// into a free slot's pinned staging (the rows may be reused as soon as it
+// returns: Java heap arrays are pinned only for the call) and queues H2D ->
+// kernel -> D2H on the slot's stream; collect waits for that operation and
+// copies its output rows (and chained CRCs) out. While round r runs on the
+// GPU the caller reads round r + 1 and submits it, so successive rounds
+// overlap (Encoder.java:421-453 runs them back to back).
+
+hrs_status async_slot(hrs_codec* c, hrs_codec::AsyncSlot& a, size_t bytes) {
+  if (!a.stream) {
+    hipError_t e = hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(c, e, "hipStreamCreate");
+    e = hipEventCreateWithFlags(&a.done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+  }
+  if (a.bytes >= bytes) return HRS_OK;
+  (void)hipStreamSynchronize(a.stream);
+  if (a.dev) (void)hipFree(a.dev);
+  if (a.pin) (void)hipHostFree(a.pin);
+  a.dev = nullptr;
+  a.pin = nullptr;
+  a.bytes = 0;
+  hipError_t e = hipMalloc(&a.dev, bytes);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  e = hipHostMalloc(&a.pin, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  a.bytes = bytes;
+  return HRS_OK;
+}
+
+hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_t* m, int nout, int nin,
+                             const uint8_t* const* in_rows, size_t len, bool static_kp, int crc_mode) {
+  const int ncrc = crc_mode == kCrcEncode ? nin + nout : crc_mode == kCrcOutputs ? nout : 0;
+  std::vector<int> slot_of(nin, -1);
+  int nlive = 0;
+  for (int i = 0; i < nin; ++i) {
+    bool any = crc_mode == kCrcEncode;
+    for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
+    if (!any) continue;
+    if (!in_rows[i]) return fail(c, HRS_EINVAL, "input row %d is NULL", i);
+    slot_of[i] = nlive++;
+  }
+  const size_t pitch = pitch_for(len);
+  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
+  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
+  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(len, 1, ncrc) : crc_off;
+  hrs_status st = async_slot(c, a, need);
+  if (st != HRS_OK) return st;
+  std::vector<hrs::CopyJob> jobs;
+  for (int i = 0; i < nin; ++i)
+    if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len});
+  hrs::CopyPool::instance().run(jobs);
+  if (nlive > 0) {
+    hipError_t e = hipMemcpyAsync(a.dev, a.pin, pitch * (nlive - 1) + len, hipMemcpyHostToDevice, a.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
+  }
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? a.dev + pitch * slot_of[i] : nullptr;
+  for (int o = 0; o < nout; ++o) dout[o] = a.dev + pitch * (nlive + o);
+  uint32_t* dcrc = reinterpret_cast<uint32_t*>(a.dev + crc_off);
+  uint32_t* draw = reinterpret_cast<uint32_t*>(a.dev + raw_off);
+  if (crc_mode == kCrcEncode)
+    st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, a.stream, draw);
+  else
+    st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, a.stream, static_kp);
+  if (st != HRS_OK) return st;
+  if (crc_mode == kCrcOutputs) {
+    std::vector<size_t> strides(nout, 0);
+    st = run_crc(c, dout.data(), strides.data(), nout, len, 1, nullptr, dcrc, a.stream, draw);
+    if (st != HRS_OK) return st;
+  }
+  const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + len;
+  hipError_t e = hipMemcpyAsync(a.pin + pitch * nlive, a.dev + pitch * nlive, back, hipMemcpyDeviceToHost, a.stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+  e = hipEventRecord(a.done, a.stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  a.nout = nout;
+  a.nlive = nlive;
+  a.ncrc = ncrc;
+  a.len = len;
+  a.pitch = pitch;
+  a.crc_off = crc_off;
+  a.queued = true;
+  return HRS_OK;
+}
+
+hrs_status async_submit(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows, size_t len,
+                        bool static_kp, int crc_mode, uint64_t* ticket) {
+  if (!ticket) return fail(c, HRS_EINVAL, "ticket is NULL");
+  *ticket = 0;
+  int free_slot = -1;
+  for (int i = 0; i < hrs::kAsyncSlots && free_slot < 0; ++i)
+    if (!c->async[i].busy) free_slot = i;
+  if (free_slot < 0)
+    return fail(c, HRS_EINVAL, "all %d asynchronous slots hold uncollected operations: collect one first",
+                hrs::kAsyncSlots);
+  hrs_codec::AsyncSlot& a = c->async[free_slot];
+  const int ncrc = crc_mode == kCrcEncode ? nin + nout : crc_mode == kCrcOutputs ? nout : 0;
+  a.queued = false;
+  a.nout = nout;
+  a.ncrc = ncrc;
+  a.len = len;
+  if (len > 0 && nout > 0) {
+    DeviceGuard g(c->device);
+    if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+    const hrs_status st = async_submit_impl(c, a, m, nout, nin, in_rows, len, static_kp, crc_mode);
+    if (st != HRS_OK) {  // leave nothing in flight in a slot marked free
+      if (a.stream) (void)hipStreamSynchronize(a.stream);
+      a.queued = false;
+      return st;
+    }
+  }
+  a.busy = true;
+  a.ticket = ++c->async_tickets;
+  *ticket = a.ticket;
+  return HRS_OK;
+}
+
+}  // namespace hrs::api
+
+using namespace hrs::api;
+
+extern "C" {
+
+hrs_status hrs_encode(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  if (!c) return HRS_EINVAL;
+  if (!inputs || !outputs) return fail(c, HRS_EINVAL, "inputs/outputs is NULL");
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, static_encode_family(c));
+}
+
+hrs_status hrs_encode_crc(hrs_codec* c, const uint8_t* const* inputs, uint8_t* const* outputs, size_t len,
+                          const uint32_t* crc_in, uint32_t* crc_out) {
+  if (!c) return HRS_EINVAL;
+  if (!inputs || !outputs || !crc_out) return fail(c, HRS_EINVAL, "inputs/outputs/crc_out is NULL");
+  HostCrc crc;
+  crc.mode = kCrcEncode;
+  crc.in = crc_in;
+  crc.out = crc_out;
+  return host_apply(c, c->g.data(), c->p, c->k, inputs, outputs, len, static_encode_family(c), crc);
+}
+
+hrs_status hrs_decode_crc(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs,
+                          const int* erased, int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len,
+                          const uint32_t* crc_in, uint32_t* crc_out) {
+  if (!c) return HRS_EINVAL;
+  (void)to_read;
+  if (!read_bufs || (ne > 0 && (!write_bufs || !erased || !crc_out)) || ne < 0 || nn < 0 || nr < 0 ||
+      (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) ||
+      (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+    return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
+  if (ne == 0) return HRS_OK;
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d, to_read, to_read ? nr : -1);
+  if (st != HRS_OK) return st;
+  HostCrc crc;
+  crc.mode = kCrcOutputs;
+  crc.in = crc_in;
+  crc.out = crc_out;
+  return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false, crc);
+}
+
+hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                      int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len) {
+  if (!c) return HRS_EINVAL;
+  (void)to_read;
+  if (!read_bufs || (ne > 0 && (!write_bufs || !erased)) || ne < 0 || nn < 0 || nr < 0 || (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) || (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+    return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
+  if (ne == 0 && c->kind == HRS_CODE_RS) return HRS_OK;
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d, to_read, to_read ? nr : -1);
+  if (st != HRS_OK) return st;
+  return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
+}
+
+hrs_status hrs_decode3(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
+                       int ne, size_t len) {
+  if (!c) return HRS_EINVAL;
+  if (ne < 0 || (ne > 0 && (!read_bufs || !write_bufs || !erased))) return fail(c, HRS_EINVAL, "bad decode3 arguments");
+  if (c->kind == HRS_CODE_XOR) {  // XORCode.decodeBulk 3-arg == 5-arg (XORCode.java:140-145)
+    std::vector<uint8_t> tmp;
+    const uint8_t* d = nullptr;
+    hrs_status st = decode5_matrix(c, erased, ne, nullptr, 0, read_bufs, tmp, &d);
+    if (st != HRS_OK) return st;
+    return host_apply(c, d, ne, c->n, read_bufs, write_bufs, len, false);
+  }
+  if (c->kind == HRS_CODE_NRS || c->kind == HRS_CODE_SRC)  // only ReedSolomonCode / XORCode have it
+    return fail(c, HRS_EINVAL, "decodeBulk(readBufs, writeBufs, erasedLocations) is not supported by this code");
+  if (ne == 0) return HRS_OK;  // ReedSolomonCode.java:170-172
+  if (ne > c->p) return fail(c, HRS_EINVAL, "%d erasures > parity size %d", ne, c->p);  // errSignature[p]
+  hrs_status st;
+  const std::vector<uint8_t>* d = cached_decode_matrix(c, erased, ne, erased, ne, 0, &st);
+  if (!d) return st;
+  return host_apply(c, d->data(), ne, c->n, read_bufs, write_bufs, len, false);
+}
+
+hrs_status hrs_encode_submit(hrs_codec* c, const uint8_t* const* inputs, size_t len, int checksums, uint64_t* ticket) {
+  if (!c) return HRS_EINVAL;
+  if (!inputs) return fail(c, HRS_EINVAL, "inputs is NULL");
+  return async_submit(c, c->g.data(), c->p, c->k, inputs, len, static_encode_family(c),
+                      checksums ? kCrcEncode : kCrcNone, ticket);
+}
+
+hrs_status hrs_decode_submit(hrs_codec* c, const uint8_t* const* read_bufs, const int* erased, int ne,
+                             const int* to_read, int nr, const int* ntr, int nn, size_t len, int checksums,
+                             uint64_t* ticket) {
+  if (!c) return HRS_EINVAL;
+  if (!read_bufs || ne < 0 || nn < 0 || nr < 0 || (ne > 0 && !erased) || (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) ||
+      (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+    return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  if (ne > 0) {
+    hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, read_bufs, tmp, &d, to_read, to_read ? nr : -1);
+    if (st != HRS_OK) return st;
+  }
+  return async_submit(c, d, ne, c->n, read_bufs, ne > 0 ? len : 0, false, checksums ? kCrcOutputs : kCrcNone, ticket);
+}
+
+hrs_status hrs_collect(hrs_codec* c, uint64_t ticket, uint8_t* const* outputs, uint32_t* crc_io) {
+  if (!c) return HRS_EINVAL;
+  hrs_codec::AsyncSlot* a = nullptr;
+  for (auto& s : c->async)
+    if (s.busy && s.ticket == ticket) a = &s;
+  if (!a) return fail(c, HRS_EINVAL, "no uncollected operation with ticket %llu", static_cast<unsigned long long>(ticket));
+  if (a->nout > 0 && a->len > 0 && !outputs) return fail(c, HRS_EINVAL, "outputs is NULL");
+  if (a->ncrc > 0 && !crc_io) return fail(c, HRS_EINVAL, "crc_io is NULL for a checksummed operation");
+  for (int o = 0; o < a->nout && a->len > 0; ++o)
+    if (!outputs[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  hrs_status st = HRS_OK;
+  if (a->queued) {
+    hipError_t e = hipEventSynchronize(a->done);
+    if (e != hipSuccess) {
+      // the slot's H2D / kernel / D2H may still be in flight: drain its stream
+      // before the slot is marked free, so the next submit cannot refill
+      // staging the DMA engine is still using
+      st = hip_fail(c, e, "hipEventSynchronize");
+      DeviceGuard g(c->device);
+      (void)hipStreamSynchronize(a->stream);
+    }
+  }
+  if (st == HRS_OK && a->queued) {
+    std::vector<hrs::CopyJob> jobs;
+    for (int o = 0; o < a->nout; ++o) jobs.push_back({outputs[o], a->pin + a->pitch * (a->nlive + o), a->len});
+    hrs::CopyPool::instance().run(jobs);
+  }
+  if (st == HRS_OK && a->ncrc > 0 && a->queued) {  // CRC32.update chaining: crc = Z_len(crc) ^ crc(cell)
+    const uint32_t* part = reinterpret_cast<const uint32_t*>(a->pin + a->crc_off);
+    const hrs::crc::Mat& z = crc_zmat(c, a->len);
+    for (int r = 0; r < a->ncrc; ++r) crc_io[r] = hrs::crc::apply(z, crc_io[r]) ^ part[r];
+  }
+  a->busy = false;
+  a->queued = false;
+  return st;
+}
+
+hrs_status hrs_wait(hrs_codec* c, uint64_t ticket) {
+  if (!c) return HRS_EINVAL;
+  for (auto& s : c->async)
+    if (s.busy && s.ticket == ticket) {
+      if (!s.queued) return HRS_OK;
+      hipError_t e = hipEventSynchronize(s.done);
+      return e == hipSuccess ? HRS_OK : hip_fail(c, e, "hipEventSynchronize");
+    }
+  return fail(c, HRS_EINVAL, "no uncollected operation with ticket %llu", static_cast<unsigned long long>(ticket));
+}
+
+hrs_status hrs_ticket_shape(const hrs_codec* c, uint64_t ticket, int* num_outputs, size_t* len, int* num_crcs) {
+  if (!c) return HRS_EINVAL;
+  for (const auto& s : c->async)
+    if (s.busy && s.ticket == ticket) {
+      if (num_outputs) *num_outputs = s.nout;
+      if (len) *len = s.len;
+      if (num_crcs) *num_crcs = s.ncrc;
+      return HRS_OK;
+    }
+  return HRS_EINVAL;
+}
+
+int hrs_pending(const hrs_codec* c) {
+  if (!c) return -1;
+  int n = 0;
+  for (const auto& s : c->async) n += s.busy;
+  return n;
+}
+
+}  // extern "C"

@@ -59,6 +59,13 @@ hipError_t launch_bytewise(const RowArgs& a, hipStream_t s);
 hipError_t launch_xor(const RowArgs& a, hipStream_t s);
 int device_cu_count();  // CUs of the current device (cached)
 
+// The last kernel this thread launched, named as rocprofv3 demangles it
+// (e.g. "encode_static_kernel<10, 4>"): the host units copy it onto the
+// handle after a call's main launch (hrs_last_kernel), so a benchmark can
+// look up the PMC traffic of the kernel the run actually used.
+void note_kernel(const char* name);
+const char* last_kernel();
+
 // ---- heterogeneous batches: one erasure pattern per stripe (hrs_decode_batch_dev)
 
 constexpr int kBatchMaxIn = 32;  // > 16 inputs (or > 8 with 6-8 outputs): batch_stream_kernel

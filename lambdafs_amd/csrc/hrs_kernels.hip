@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "hrs_device.hpp"
 #include "hrs_launch.hpp"
@@ -167,6 +168,7 @@ __global__ void __launch_bounds__(kBlockThreads) bytewise_kernel(const RowArgs a
 template <int K, int P>
 hipError_t launch_static(const RowArgs& a, hipStream_t s) {
   auto kern = encode_static_kernel<K, P>;
+  note_kernel_t("encode_static_kernel", K, P);
   const unsigned g = stream_grid(a.ntasks);
   hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
@@ -175,6 +177,7 @@ hipError_t launch_static(const RowArgs& a, hipStream_t s) {
 template <int K, int P>
 hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
   auto kern = encode_cauchy_kernel<K, P>;
+  note_kernel_t("encode_cauchy_kernel", K, P);
   const unsigned g = stream_grid(a.ntasks);
   hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
@@ -183,6 +186,12 @@ hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
 }  // namespace
 
 int device_cu_count() { return device_cus(); }
+
+namespace {
+thread_local std::string t_last_kernel;
+}
+void note_kernel(const char* name) { t_last_kernel = name; }
+const char* last_kernel() { return t_last_kernel.c_str(); }
 
 hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipStream_t s, bool* handled) {
   *handled = true;
@@ -203,6 +212,7 @@ hipError_t launch_static_encode(int family, int k, int p, const RowArgs& a, hipS
 template <int NINB>
 hipError_t launch_xor_n(const RowArgs& a, hipStream_t s) {
   auto kern = xor_kernel<NINB>;
+  note_kernel_t("xor_kernel", NINB);
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }
@@ -217,6 +227,7 @@ hipError_t launch_xor(const RowArgs& a, hipStream_t s) {
 
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s) {
   const unsigned g = grid_for(bytewise_kernel, kBlockThreads, a.ntasks);
+  note_kernel("bytewise_kernel");
   hipLaunchKernelGGL(bytewise_kernel, dim3(g), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }

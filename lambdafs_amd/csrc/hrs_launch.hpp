@@ -6,11 +6,27 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 
 #include "hrs_internal.hpp"
 
 namespace hrs {
 
+// note_kernel with the template arguments spelled as rocprofv3 prints them:
+// note_kernel_t("bitsliced_pipe_kernel", 1, 12) -> "bitsliced_pipe_kernel<1, 12>".
+inline void kname_arg(std::string& s, int v) { s += std::to_string(v); }
+inline void kname_arg(std::string& s, bool v) { s += v ? "true" : "false"; }
+inline void kname_arg(std::string& s, const char* v) { s += v; }
+template <typename... T>
+inline void note_kernel_t(const char* base, T... v) {
+  std::string s(base);
+  if constexpr (sizeof...(T) > 0) {
+    const char* sep = "<";
+    ((s += sep, kname_arg(s, v), sep = ", "), ...);
+    s += '>';
+  }
+  note_kernel(s.c_str());
+}
 
 // CU count per device, cached; handles on several host threads may race to
 // fill it (same value), hence the relaxed atomics.

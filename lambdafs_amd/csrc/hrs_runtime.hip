@@ -212,8 +212,13 @@ bool use_pipe() {
 template <int NOUT, int NINB>
 hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_kernel<NOUT, NINB>;
+  const char* name = "bitsliced_kernel";
   if constexpr (kPipeFits<NOUT, NINB>)
-    if (use_pipe()) kern = bitsliced_pipe_kernel<NOUT, NINB>;
+    if (use_pipe()) {
+      kern = bitsliced_pipe_kernel<NOUT, NINB>;
+      name = "bitsliced_pipe_kernel";
+    }
+  note_kernel_t(name, NOUT, NINB);
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
@@ -233,6 +238,7 @@ hipError_t launch_bits(const RowArgs& a, hipStream_t s) {
 template <int NOUT>
 hipError_t launch_stream_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_stream_kernel<NOUT, kStreamGroup>;
+  note_kernel_t("bitsliced_stream_kernel", NOUT, kStreamGroup);
   const int per_cu = NOUT >= 4 ? 3 : 2;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();

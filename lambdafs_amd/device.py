@@ -193,3 +193,34 @@ def crc32_rows(code, row_views, crc_in=None):
     code._check(_lib.lib().hrs_crc32_dev(code._handle(), rows, len(row_views), stride, L, S, cin, out.data_ptr(),
                                          _stream(ref)))
     return out
+
+
+def probe_copy(src, dst, blocks_per_cu=4):
+    """HBM ceiling probe (include/hrs_probe.h): dst <- src, both contiguous
+    device tensors of the same byte size, by the nontemporal 16-byte
+    grid-stride copy kernel at `blocks_per_cu` blocks per CU, on the
+    current stream. Diagnostic: bench.py's copy_peak."""
+    nbytes = src.numel() * src.element_size()
+    if (not src.is_cuda or not dst.is_cuda or not src.is_contiguous() or not dst.is_contiguous()
+            or dst.numel() * dst.element_size() != nbytes):
+        raise ValueError("probe_copy needs two contiguous device tensors of equal size")
+    st = _lib.lib().hrs_probe_copy(src.data_ptr(), dst.data_ptr(), nbytes, int(blocks_per_cu), _stream(src))
+    _lib.check(st)
+
+
+def probe_read(src, sink, blocks_per_cu=4):
+    """HBM read-only probe (hrs_probe_read): reads the contiguous device
+    tensor `src` once; `sink` is a device tensor of >= 4 KiB (never written
+    in practice)."""
+    if not src.is_cuda or not src.is_contiguous() or sink.numel() * sink.element_size() < 4096:
+        raise ValueError("probe_read needs a contiguous device tensor and a 4 KiB device sink")
+    _lib.check(_lib.lib().hrs_probe_read(src.data_ptr(), src.numel() * src.element_size(), int(blocks_per_cu),
+                                         sink.data_ptr(), _stream(src)))
+
+
+def probe_write(dst, blocks_per_cu=4):
+    """HBM write-only probe (hrs_probe_write): writes the contiguous device tensor `dst` once."""
+    if not dst.is_cuda or not dst.is_contiguous():
+        raise ValueError("probe_write needs a contiguous device tensor")
+    _lib.check(_lib.lib().hrs_probe_write(dst.data_ptr(), dst.numel() * dst.element_size(), int(blocks_per_cu),
+                                          _stream(dst)))

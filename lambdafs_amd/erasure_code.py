@@ -229,6 +229,11 @@ class _HipErasureCode(ErasureCode):
         self._check(_lib.lib().hrs_set_kernel_mode(self._handle(), int(mode)))
 
     # -- matrices (host)
+    def lastKernel(self):
+        """Main kernel of this handle's latest coding call, as rocprofv3 names
+        it (hrs_last_kernel); "" before any device work."""
+        return _lib.lib().hrs_last_kernel(self._handle()).decode()
+
     def encodeMatrix(self):
         g = np.zeros((self._p, self._k), dtype=np.uint8)
         self._check(_lib.lib().hrs_encode_matrix(self._handle(), g.ctypes.data))

@@ -34,7 +34,9 @@
  * Critical regions: no JNI call runs between the first
  * GetPrimitiveArrayCritical and the last ReleasePrimitiveArrayCritical; the
  * region lasts one engine call (~0.45 ms for an RS(10,4) 1 MiB-cell encode,
- * DESIGN.md §7), during which a JVM without region pinning defers GC.
+ * DESIGN.md §7), during which a JVM without region pinning defers GC. collect
+ * waits for its round (hrs_wait) before it pins anything, so its region is
+ * only the copy out of pinned staging.
  *
  * Build: make jni (this header set) or, with a JDK,
  *   gcc -O2 -fPIC -shared -DHRS_SYSTEM_JNI -I$JAVA_HOME/include -I$JAVA_HOME/include/linux \
@@ -490,7 +492,7 @@ done:
   return (jlong)ticket;
 }
 
-/* hrs_collect: waits for the round, copies its output rows into `outputs`
+/* hrs_wait, then hrs_collect: copies the round's output rows into `outputs`
  * (p rows / one per erased location, each at least the round's length); a
  * checksummed round continues the running CRC32s in `crcs` (k + p / one per
  * erased location) in place. */
@@ -504,6 +506,16 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_collect(JNIEnv* en
   if (hrs_ticket_shape(c, (uint64_t)ticket, &nout, &len, &ncrc) != HRS_OK) {
     throw_msg(env, kIAE, "no uncollected operation with ticket %lld", (long long)ticket);
     return;
+  }
+  /* wait for the round BEFORE pinning the output rows: the critical region
+   * below then covers only the copy out of the slot's staging, not a GPU
+   * wait that may queue behind up to three other rounds */
+  {
+    const hrs_status ws = hrs_wait(c, (uint64_t)ticket);
+    if (ws != HRS_OK) {
+      throw_status(env, ws, c);
+      return;
+    }
   }
   if (open_frame(env)) return;
   uint32_t crc[MAX_ROWS];

@@ -31,6 +31,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <dlfcn.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <unistd.h>
@@ -292,9 +293,24 @@ static void JNICALL f_SetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, j
   memcpy(ints_of(a) + start, buf, (size_t)len * sizeof(jint));
 }
 
+/* hrs_wait interposed (this executable's definition wins over libhrs's for
+ * the shim): records the ticket the shim waited on last, so the fake JVM can
+ * check that collect pins its output rows only after its round completed,
+ * i.e. that no critical region covers a GPU wait. */
+static uint64_t g_waited_ticket = 0;
+static uint64_t g_collect_ticket = 0; /* nonzero while a collect call runs */
+hrs_status hrs_wait(hrs_codec* c, uint64_t t) {
+  static hrs_status (*real)(hrs_codec*, uint64_t) = NULL;
+  if (!real) *(void**)&real = dlsym(RTLD_NEXT, "hrs_wait");
+  g_waited_ticket = t;
+  return real ? real(c, t) : HRS_EDEVICE;
+}
+
 static void* JNICALL f_GetPrimitiveArrayCritical(JNIEnv* env, jarray a, jboolean* is_copy) {
   (void)env;
   enter("GetPrimitiveArrayCritical", 0, 1);
+  if (g_collect_ticket && g_waited_ticket != g_collect_ticket)
+    violation("collect pinned a row before waiting for ticket %llu", (unsigned long long)g_collect_ticket);
   if (!a || (a->kind != K_BYTES && a->kind != K_INTS)) {
     violation("GetPrimitiveArrayCritical on a non-primitive array");
     return NULL;
@@ -397,6 +413,14 @@ static const char* thrown(void) { return vm.pending ? vm.exc_class : ""; }
     begin_native_call();            \
     expr;                           \
     end_native_call(label);         \
+  } while (0)
+
+/* HrsNative.collect with the wait-before-pin check armed (hrs_wait above). */
+#define COLLECT(label, ticket, outs, crcs)                              \
+  do {                                                                  \
+    g_collect_ticket = (uint64_t)(ticket);                              \
+    CALL(label, NS(collect)(env, NULL, h, (ticket), (outs), (crcs)));   \
+    g_collect_ticket = 0;                                               \
   } while (0)
 
 #define EXPECT_THROWN(label, cls, expr)                                                      \
@@ -717,7 +741,7 @@ static int gpu_checks(void) {
       if (r >= 1) {
         const int q = r - 1;
         jobjectArray out = rows(p, Lr, 0);
-        CALL("collect", NS(collect)(env, NULL, h, tk[q], out, run));
+        COLLECT("collect", tk[q], out, run);
         ok &= !vm.pending;
         uint8_t* ri[10];
         uint8_t* ro[4];
@@ -745,7 +769,7 @@ static int gpu_checks(void) {
          td = NS(decodeSubmit)(env, NULL, h, cw, new_ints(1, er1), new_ints(10, tr1), new_ints(4, ntr1), L, JNI_TRUE));
     jobjectArray dw = rows(1, L, 0);
     jintArray dc = new_ints(1, NULL);
-    CALL("collect decode", NS(collect)(env, NULL, h, td, dw, dc));
+    COLLECT("collect decode", td, dw, dc);
     expect(!vm.pending && memcmp(bytes_of(row(dw, 0)), bytes_of(row(in, 0)), (size_t)L) == 0 &&
                (uint32_t)ints_of(dc)[0] == zcrc(0, bytes_of(row(in, 0)), (size_t)L),
            "async decode round + repaired CRC");
@@ -753,7 +777,7 @@ static int gpu_checks(void) {
     jlong t5[5];
     for (int r = 0; r < 4; ++r) CALL("encodeSubmit x4", t5[r] = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
     EXPECT_THROWN("fifth outstanding round", kIAE, t5[4] = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
-    for (int r = 3; r >= 0; --r) CALL("collect out of order", NS(collect)(env, NULL, h, t5[r], rows(p, 4096, 0), NULL));
+    for (int r = 3; r >= 0; --r) COLLECT("collect out of order", t5[r], rows(p, 4096, 0), NULL);
     expect(!vm.pending, "collect in any order");
   }
   CALL("destroy", NS(destroy)(env, NULL, h));

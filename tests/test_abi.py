@@ -1,5 +1,5 @@
 """CPU tests of the product boundary: libhrs.so loads, exports every symbol
-include/hrs.h declares, and its host-side logic (encode/decode matrices,
+include/*.h declares (and nothing else), and its host-side logic (encode/decode matrices,
 locationsToReadForDecode, argument and error handling) agrees with the
 oracle. No coding call runs here (no GPU in this container)."""
 import ctypes
@@ -18,9 +18,12 @@ NONE = -2  # HRS_DEVICE_NONE
 
 
 def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "hrs.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(hrs_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in ("hrs.h", "hrs_probe.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(hrs_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -31,6 +34,17 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert set(names) == set(_lib.EXPORTS)
     assert b"gfx950" in _lib.lib().hrs_version()
+
+
+def test_library_exports_only_the_c_abi():
+    """The version script (lambdafs_amd/csrc/libhrs.map) keeps the C++
+    internals local: the dynamic symbol table holds the declared hrs_*
+    entry points (plus HIP's per-TU __hip_cuid_ markers) and nothing else."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    syms = {ln.split()[-1] for ln in out.stdout.splitlines() if ln.strip()}
+    extra = {s for s in syms if not s.startswith("__hip_cuid_")} - set(declared_symbols())
+    assert not extra, sorted(extra)[:10]
 
 
 def test_library_is_gfx950_code_object():

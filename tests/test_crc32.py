@@ -86,3 +86,27 @@ def test_encode_then_block_checksums(cuda):
     for s in (0, S - 1):
         for r in range(k + p):
             assert _u32(crcs[s, r]) == zlib.crc32(host[s, r].tobytes())
+
+
+@pytest.mark.gpu
+def test_fold_table_cache_eviction_across_streams(cuda):
+    """More distinct row lengths than the fold-table cache holds (64): the
+    least recently used entry is evicted after the event behind its latest
+    fold, with calls queued on two streams and never synchronized in between;
+    lengths evicted early come back (rebuilt) at the end. Every CRC vs zlib."""
+    torch = cuda
+    code = HipReedSolomonCode(10, 4)
+    lens = [4096 + 48 * i for i in range(72)] + [4096, 4096 + 48]
+    rng = np.random.default_rng(77)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = []
+    for i, L in enumerate(lens):
+        rows = torch.from_numpy(rng.integers(0, 256, (3, L), dtype=np.uint8)).cuda()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(streams[i % 2]):
+            jobs.append((rows, device.crc32_rows(code, [rows[r:r + 1] for r in range(3)])))
+    torch.cuda.synchronize()
+    for rows, got in jobs:
+        host = rows.cpu().numpy()
+        want = [zlib.crc32(host[r].tobytes()) for r in range(3)]
+        assert [int(x) & 0xFFFFFFFF for x in got[0].tolist()] == want

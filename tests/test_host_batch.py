@@ -97,9 +97,10 @@ def test_encode_then_decode_batch_host_round_trip(cuda, pinned):
 
 
 def test_decode_batch_host_wide_and_src_codes(cuda):
-    """Patterns beyond the batch kernel (RS(20,8) with 6-8 losses next to
-    1-loss stripes: per-stripe launches) and the src code's local groups
-    (only the group crosses PCIe)."""
+    """Wide patterns in the streaming batch kernel (RS(20,8) with 6-8 losses
+    next to 1-loss stripes: up to 20 survivors, within kBatchMaxIn = 32, so
+    batch_stream_kernel runs them in one launch) and the src code's local
+    groups (only the group crosses PCIe)."""
     torch = cuda
     k, p, S, L = 20, 8, 12, 40000
     n = k + p
@@ -142,3 +143,33 @@ def test_host_batch_errors(cuda):
         device.decode_batch_host(code, st, er, out[:, :1])
     with pytest.raises(ValueError):
         device.decode_batch_host(code, st[:, :13], er, out[:, :1])
+
+
+def test_decode_batch_host_per_stripe_fallback_over_32_survivors(cuda):
+    """Patterns with more live survivors than the batch kernels hold
+    (kBatchMaxIn = 32): RS(40,6) repairs read 40 survivors, so the host batch
+    takes its per-stripe path (ps.fused == false): the rows each stripe moves
+    come from its decode matrix's nonzero columns, and one run_apply per
+    stripe repairs it. Mixed with 1-loss stripes of the same batch; pinned and
+    pageable; every repaired cell vs the oracle's decodeBulk."""
+    torch = cuda
+    k, p, S, L = 40, 6, 9, 8192 + 48
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=0)
+    for pinned in (True, False):
+        st = _alloc(torch, (S, n, L), pinned)
+        st[:, :p] = 0
+        st[:, p:] = np.random.default_rng(11).integers(0, 256, (S, k, L), dtype=np.uint8)
+        device.encode_batch_host(code, st)
+        er = _patterns(random.Random(13), S, n, 6, lambda s: (1, 3, 6)[s % 3])
+        out = _alloc(torch, (S, 6, L), pinned)
+        device.decode_batch_host(code, st, er, out)
+        for s in range(S):
+            lost = [int(x) for x in er[s] if x >= 0]
+            to_read = sorted(C.locations_to_read(k, p, lost))
+            ntr = [x for x in range(n) if x not in to_read]
+            reads = [st[s, j] if j in to_read else np.zeros(L, np.uint8) for j in range(n)]
+            ref = C.decode_bulk5(k, p, reads, lost, to_read, ntr)
+            for t in range(len(lost)):
+                assert np.array_equal(out[s, t], ref[t]), (pinned, s, lost)
+                assert np.array_equal(out[s, t], st[s, lost[t]]), (pinned, s, lost)

@@ -19,15 +19,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
-def bench_line(nproc, stripes, port):
+def bench_line(nproc, stripes, port, self_launch=False):
     common = ["--stripes", str(stripes), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-e2e"]
     if nproc == 1:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"] + common
+    elif self_launch:  # bench.py starts its own torch.distributed.run child (no launcher here)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--dist-backend", "gloo"] + common
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                "--gpus", str(nproc), "--dist-backend", "gloo"] + common
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MASTER_ADDR"] = "127.0.0.1"
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -42,3 +45,15 @@ def test_two_ranks_match_one_rank_stripe_for_stripe(cuda):
     assert one["parity_sha256"]["blocks"] == two["parity_sha256"]["blocks"]
     assert set(one["parity_sha256"]["blocks"]) == {"0", "256"}
     assert two["value"] > 0 and two["scaling"] == "weak"
+
+
+def test_gpus_two_without_launcher_runs_two_ranks(cuda):
+    """`bench.py --gpus 2` with no launcher must start two
+    ranks itself (a torch.distributed.run child), report n_gpus 2 and print
+    the same per-block digests as the 1-rank run over the same stripes."""
+    one = bench_line(1, 512, 0)
+    two = bench_line(2, 256, 0, self_launch=True)
+    assert two["n_gpus"] == 2 and two["config"]["stripes_total"] == 512
+    assert one["parity_sha256"]["blocks"] == two["parity_sha256"]["blocks"]
+    assert one["parity_sha256"]["decode_blocks"] == two["parity_sha256"]["decode_blocks"]
+    assert two["parity_vs_oracle"] == {"blocks": 4, "match": True}
