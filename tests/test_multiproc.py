@@ -83,3 +83,65 @@ def test_stripe_range_partition():
             assert spans[0][0] == 0 and spans[-1][1] == total
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - lo for lo, h in spans) - min(h - lo for lo, h in spans) <= 1
+
+
+def _bench_flow_worker(r, nranks, port, outdir):
+    """bench.py's collective sequence under gloo with host-only handles:
+    matrix broadcasts, the barriers and max-over-ranks around the timed
+    region, the all-ok checks, the per-block digest gathers (parity, decode,
+    config-5 repairs) and their comparison with the oracle's digests, the
+    e2e leg's reductions, and the final barrier — in bench.py's order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(nranks))
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from lambdafs_amd import HipReedSolomonCode, parallel
+    dist.init_process_group("gloo", rank=r, world_size=nranks)
+    try:
+        k, p = 10, 4
+        code = HipReedSolomonCode(k, p, device=-2)
+        erased = [p]
+        to_read = sorted(code.locationsToReadForDecode(erased))
+        ntr = [x for x in range(k + p) if x not in to_read]
+        G = parallel.broadcast_matrix(code.encodeMatrix())
+        D = parallel.broadcast_matrix(code.decodeMatrix(erased, ntr))
+        parallel.barrier()
+        parallel.barrier()
+        elapsed = parallel.max_over_ranks(1.0 + r / 10)
+        ok = parallel.all_ok(True) and parallel.all_ok(True)
+        golden = bench.load_golden()
+        S, g0 = 1024, r * 1024
+        # each rank's digests: the oracle's own blocks for its global range
+        par = {key: v for key, v in golden["config3"]["parity"].items() if g0 <= int(key) < g0 + S}
+        dec = {key: v for key, v in golden["config3"]["decode"].items() if g0 <= int(key) < g0 + S}
+        digs = {"parity": bench.gather_blocks(par, nranks), "decode": bench.gather_blocks(dec, nranks)}
+        vs = bench.compare_blocks(digs, golden["config3"], ("parity", "decode"))
+        # e2e leg (config 5, 512 stripes per rank)
+        t = [parallel.max_over_ranks(float(r + i)) for i in range(3)]
+        ok_e2e = parallel.all_ok(r != nranks + 1)
+        rep = {key: v for key, v in golden["config5"]["repaired"].items() if r * 512 <= int(key) < (r + 1) * 512}
+        rep_all = bench.gather_blocks(rep, nranks)
+        vs5 = bench.compare_blocks({"repaired": rep_all}, golden["config5"], ("repaired",))
+        dist.barrier()
+        np.savez(os.path.join(outdir, f"flow{r}.npz"), G=G, D=D, elapsed=elapsed, ok=ok and ok_e2e,
+                 nblocks=vs["blocks"], nrep=vs5["blocks"], t=np.array(t), keys=np.array(sorted(digs["parity"])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_collective_flow_world8(tmp_path):
+    """bench.py's multi-rank control flow with 8 ranks
+    (gloo on CPU): no collective is rank-conditional, the per-block digests of
+    8 x 1,024 stripes gather into the full set and match the oracle's, and
+    every rank returns."""
+    port = _free_port()
+    mp.start_processes(_bench_flow_worker, args=(8, port, str(tmp_path)), nprocs=8, join=True, start_method="spawn")
+    res = [np.load(tmp_path / f"flow{r}.npz") for r in range(8)]
+    for z in res:
+        assert float(z["elapsed"]) == 1.7 and bool(z["ok"])
+        assert int(z["nblocks"]) == 64 and int(z["nrep"]) == 16  # 32 parity + 32 decode blocks; 16 repaired
+        assert z["t"].tolist() == [7.0, 8.0, 9.0]
+        assert len(z["keys"]) == 32
+        assert (z["G"] == res[0]["G"]).all() and (z["D"] == res[0]["D"]).all()

@@ -66,11 +66,9 @@ def main():
     if a.update:
         with open(a.update) as fh:
             cur = json.load(fh)
-        for k in ("encode_static_pipe_kernel<10,4>", "bitsliced_pipe_kernel<1,12>", "batch_pipe_kernel<1,12>",
-                  "encode_static_kernel<10,4>", "bitsliced_kernel<1,12>", "batch_bitsliced_kernel<1,12>",
-                  "batch_bitsliced_kernel<1,12,true>", "batch_bitsliced_kernel<1,12,false>"):
-            if k in table and "hbm_bytes_per_dispatch" in table[k]:
-                cur[k] = table[k]["hbm_bytes_per_dispatch"]
+        for k, t in table.items():  # every libhrs kernel the profiled run launched (bench.py looks them up by name)
+            if "hbm_bytes_per_dispatch" in t:
+                cur[k] = t["hbm_bytes_per_dispatch"]
         cur["_note"] = (cur.get("_note", "").split("; source")[0] + "; source " + a.profile_dir + "/pmc_*/")
         with open(a.update, "w") as fh:
             json.dump(cur, fh, indent=1)
