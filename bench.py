@@ -53,8 +53,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)  # ~0.5 s timed at N=1: long enough for an SMI sampler to see it
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU (weak scaling)")
     ap.add_argument("--strong", action="store_true",
                     help="--stripes is the job total, split into contiguous ranges over the ranks")

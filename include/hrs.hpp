@@ -181,6 +181,10 @@ class HipCode : public ErasureCode {
     return t;
   }
 
+  // Blocks until the operation's GPU work is done (hrs_wait); collect then
+  // only copies.
+  void wait(uint64_t ticket) { check(hrs_wait(h_, ticket), h_); }
+
   // outputs must hold the operation's output rows exactly, and *crcs (a
   // checksummed operation only) its CRC values: hrs_collect writes that many.
   void collect(uint64_t ticket, const std::vector<uint8_t*>& outputs, std::vector<uint32_t>* crcs) {

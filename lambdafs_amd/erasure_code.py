@@ -432,6 +432,11 @@ class _HipErasureCode(ErasureCode):
                                            crc.ctypes.data if ncrc.value else None))
         return [int(x) for x in crc[: ncrc.value]] if ncrc.value else None
 
+    def wait(self, ticket):
+        """Block until a submitted operation's GPU work has completed, without
+        collecting it (hrs_wait; collect then returns without blocking)."""
+        self._check(_lib.lib().hrs_wait(self._handle(), int(ticket)))
+
     def pending(self):
         """Submitted operations not yet collected (at most 4 per codec)."""
         return int(_lib.lib().hrs_pending(self._handle()))

@@ -110,3 +110,23 @@ def test_async_argument_errors(cuda):
     # nothing erased: a decode round with no outputs
     t = code.decodeBulkAsync(ins + [np.zeros(L, np.uint8)] * p, [], list(range(k)), [])
     assert code.collect(t, []) is None
+
+
+def test_wait_then_collect(cuda):
+    """hrs_wait blocks until a round's GPU work is done without collecting it
+    (the JNI shim calls it before pinning the output rows); collect then only
+    copies. Unknown tickets and double waits are handled."""
+    k, p, L = 10, 4, 1 << 20
+    code = HipReedSolomonCode(k, p, device=0, zero_inputs_after_encode=False)
+    rng = np.random.default_rng(5)
+    rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    t = code.encodeBulkAsync(rows)
+    code.wait(t)
+    code.wait(t)  # still uncollected: waiting again is a no-op
+    assert code.pending() == 1
+    out = [np.zeros(L, np.uint8) for _ in range(p)]
+    assert code.collect(t, out) is None
+    ref = C.encode_bulk(k, p, rows)
+    assert all(np.array_equal(a, b) for a, b in zip(out, ref))
+    with pytest.raises(HrsError):
+        code.wait(t)  # collected: the ticket is gone
