@@ -86,7 +86,7 @@ struct EncodeCrcArgs {
   uint64_t nwin;      // windows per row (len / (subs * 2 KiB), len a multiple)
   uint64_t nstripes;
   uint32_t subs;      // 2 KiB sub-windows per window: 1, 2, 4, 8 or 16
-  uint32_t pad_;
+  uint32_t rep_mask;  // slicing-table copy of lane l = l & rep_mask (kCrcRep - 1; HRS_CRC_REP A/B)
   uint32_t* raw;
   const uint32_t* tables;  // kCrcLdsWordsA words (device)
 };

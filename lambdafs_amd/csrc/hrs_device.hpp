@@ -246,8 +246,10 @@ struct SliceTab {
   uint32_t lw_hi;  // 4 c | 0x10000 (tables 2, 3)
 };
 
-__device__ __forceinline__ SliceTab slice_tab(int lane) {
-  const uint32_t c4 = static_cast<uint32_t>(lane & (kCrcRep - 1)) * 4u;
+// rep_mask (A/B of the replication factor): lane l reads copy l & rep_mask;
+// kCrcRep - 1 (31) = every lane of a 32-lane group on its own bank.
+__device__ __forceinline__ SliceTab slice_tab(int lane, uint32_t rep_mask = kCrcRep - 1) {
+  const uint32_t c4 = (static_cast<uint32_t>(lane) & rep_mask) * 4u;
   return SliceTab{c4, c4 | 0x10000u};
 }
 

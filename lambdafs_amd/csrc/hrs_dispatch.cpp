@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -378,6 +379,15 @@ hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strid
   return crc_fold(c, len, nstripes * nrows, crc_in, crc_out, s, raw);
 }
 
+// Slicing-table copies the fused kernel's lanes spread over: 32 (each lane of
+// a 32-lane group on its own LDS bank); HRS_CRC_REP = 16 | 8 | 4 | 2 | 1 reads
+// fewer copies (A/B of the replication factor; read per call).
+uint32_t crc_rep_mask() {
+  const char* e = getenv("HRS_CRC_REP");
+  const int r = e ? atoi(e) : hrs::kCrcRep;
+  return (r >= 1 && r <= hrs::kCrcRep && (r & (r - 1)) == 0) ? static_cast<uint32_t>(r - 1) : hrs::kCrcRep - 1;
+}
+
 // Encode + CRC-32 of the k sources and p parities (hrs_encode_crc_dev's
 // semantics) with raw window CRCs in `raw` (crc_raw_bytes_for(len, nstripes, n)).
 hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
@@ -403,6 +413,7 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
     a.in_stride = in_stride;
     a.out_stride = out_stride;
     a.subs = subs;
+    a.rep_mask = crc_rep_mask();
     a.nwin = len / (subs * hrs::kWindowBytes);
     a.nstripes = nstripes;
     a.raw = raw;

@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(THREADS) encode_crc_kernel(const EncodeCrcArgs
   __syncthreads();
   constexpr int N = K + P;
   const int lane = threadIdx.x & 63;
-  const SliceTab slices = slice_tab(lane);
+  const SliceTab slices = slice_tab(lane, a.rep_mask);
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
   const uint64_t ntasks = a.nstripes * a.nwin;
@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
   constexpr int kGroups = (K + G - 1) / G;
   const int lane = threadIdx.x & 63;
   const uint32_t loff = static_cast<uint32_t>(lane) * 16u;
-  const SliceTab slices = slice_tab(lane);
+  const SliceTab slices = slice_tab(lane, a.rep_mask);
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
   const uint64_t ntasks = a.nstripes * a.nwin;

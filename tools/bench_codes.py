@@ -67,14 +67,20 @@ def main():
     ap.add_argument("--stripes", type=int, default=1024)
     ap.add_argument("--cell", type=int, default=1 << 20)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--codes", default="rs,nrs,xor", help="comma list of rs, nrs, xor")
     args = ap.parse_args()
     torch.manual_seed(7)
     rows = []
-    run("rs", HipReedSolomonCode(10, 4), args.stripes, args.cell, args.iters, rows)
-    run("nrs", HipNativeReedSolomonCode(10, 4), args.stripes, args.cell, args.iters, rows)
-    run("nrs", HipNativeReedSolomonCode(6, 3), args.stripes, args.cell, args.iters, rows)
-    run("xor", HipXORCode(10, 1), args.stripes, args.cell, args.iters, rows)
+    codes = args.codes.split(",")
+    if "rs" in codes:
+        run("rs", HipReedSolomonCode(10, 4), args.stripes, args.cell, args.iters, rows)
+    if "nrs" in codes:
+        run("nrs", HipNativeReedSolomonCode(10, 4), args.stripes, args.cell, args.iters, rows)
+        run("nrs", HipNativeReedSolomonCode(6, 3), args.stripes, args.cell, args.iters, rows)
+    if "xor" in codes:
+        run("xor", HipXORCode(10, 1), args.stripes, args.cell, args.iters, rows)
     for r in rows:
+        r["blocks_per_cu_env"] = os.environ.get("HRS_BLOCKS_PER_CU", "default")
         print(json.dumps(r), flush=True)
 
 
