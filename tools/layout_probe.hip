@@ -11,7 +11,8 @@
 //     base + (s / G) * GS + (s % G) * SS + r * RS + o,    o < L
 //   task t -> (stripe, window) by `order`: 0 = window-fastest (the product's
 //   t = s * nwin + w), 1 = stripe-fastest (t = w * S + s).
-// Usage: layout_probe [rounds]   -> one line per variant, medians.
+// Usage: layout_probe [rounds] [layouts|spacing]   -> one line per variant, medians.
+//   spacing: 64 KiB cells with the rows of a stripe D apart, D = 64 KiB .. 4 MiB.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -89,6 +90,7 @@ struct Var {
 
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 7;
+  const std::string mode = argc > 2 ? argv[2] : "layouts";
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const uint64_t B = 8ull << 30;
@@ -111,7 +113,19 @@ int main(int argc, char** argv) {
     else
       vars.push_back({nm, [=]() { hipLaunchKernelGGL(k100, dim3(g), dim3(256), 0, 0, a, y); }, bytes, {}});
   };
-  for (int kp = 0; kp < 2; ++kp) {
+  if (mode == "spacing") {
+    // 64 KiB cells, the rows of a stripe D apart (D a multiple of 64 KiB):
+    // G = D / 64 KiB stripes interleave in each D-sized row slot, groups of G
+    // stripes follow each other (14 * D bytes per group); ~7 GiB in total.
+    for (uint64_t dk : {64, 128, 192, 256, 512, 960, 1024, 1088, 1536, 2048, 4096}) {
+      const uint64_t D = dk << 10, G = D / K64;
+      const uint64_t groups = (7ull << 30) / (14 * D);
+      const Layout y{groups * G, K64, G, 14 * D, K64, D, 0};
+      add("L=64K rows " + std::to_string(dk) + "K apart", y, 10, 4, 2);
+      add("L=64K rows " + std::to_string(dk) + "K apart", y, 10, 1, 2);
+    }
+  }
+  for (int kp = 0; kp < (mode == "layouts" ? 2 : 0); ++kp) {
     const int p = kp == 0 ? 4 : 1;
     for (int bpc : {2}) {
       // 1: the product layout and order, 1 MiB cells (512 stripes x 14 MiB = 7 GiB)
@@ -133,10 +147,12 @@ int main(int argc, char** argv) {
       add("L=1M row-major order0", Layout{512, M, 1, M, 0, 512 * M, 0}, 10, p, bpc);
     }
   }
-  add("L=1M stripe-major order0", Layout{512, M, 1, 14 * M, 0, M, 0}, 10, 4, 1);
-  add("L=64K stripe-major order0", Layout{8192, K64, 1, 14 * K64, 0, K64, 0}, 10, 4, 1);
-  add("L=1M stripe-major order0", Layout{512, M, 1, 14 * M, 0, M, 0}, 10, 0, 2);
-  add("L=64K stripe-major order0", Layout{8192, K64, 1, 14 * K64, 0, K64, 0}, 10, 0, 2);
+  if (mode == "layouts") {
+    add("L=1M stripe-major order0", Layout{512, M, 1, 14 * M, 0, M, 0}, 10, 4, 1);
+    add("L=64K stripe-major order0", Layout{8192, K64, 1, 14 * K64, 0, K64, 0}, 10, 4, 1);
+    add("L=1M stripe-major order0", Layout{512, M, 1, 14 * M, 0, M, 0}, 10, 0, 2);
+    add("L=64K stripe-major order0", Layout{8192, K64, 1, 14 * K64, 0, K64, 0}, 10, 0, 2);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
