@@ -1,4 +1,4 @@
-// Internal interface of the CRC-32 kernels (hrs_crc.hip) for hrs_api.cpp.
+// Internal interface of the CRC-32 kernels (hrs_crc.hip, hrs_fused.hip) for hrs_dispatch.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
 

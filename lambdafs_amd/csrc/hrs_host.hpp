@@ -2,7 +2,7 @@
 // hrs_decode, the JNI path): rows arrive in pageable memory (a JNI-pinned Java
 // heap array), are copied by a few threads into pinned staging, and DMA'd from
 // there, chunk by chunk, while the GPU works on the previous chunk
-// (hrs_api.cpp: host_apply).
+// (hrs_hostpath.cpp: host_apply).
 //
 // Several codec handles may call concurrently (one codec per mapper / repair
 // thread: Encoder.java:80, Decoder.java:90, MapReduceBlockRepairManager.java:426),

@@ -1,4 +1,4 @@
-// Internal interface between the C-ABI layer (hrs_api.cpp) and the gfx950
+// Internal interface between the C-ABI host units (hrs_dispatch.cpp, hrs_batch_api.cpp) and the gfx950
 // kernels (hrs_kernels.hip).
 #pragma once
 #include <cstddef>

@@ -7,7 +7,7 @@
 // GF(2^8)-linear in the stripe bytes, so every kernel here evaluates
 //     out_o[col] = XOR_i  M[o][i] * in_i[col]        (GF(2^8) products)
 // for every byte column `col` of every stripe, with M = the encode matrix G
-// or a decode matrix D built on the host (hrs_api.cpp).
+// or a decode matrix D built on the host (hrs_matrix.cpp).
 //
 // Design (MI355X_MICROARCH.md: HBM ~6.3 TB/s achievable, VALU 64 lanes x 4
 // SIMD x 256 CU): the path is HBM-bound byte streaming, so there is no MFMA

@@ -3,7 +3,7 @@
 Parity: the oracle (orc_src_* in oracle/rs_oracle.c) transcribes the Java
 loop for loop (init's adjustment loop, groups, remainder encode, the three
 decode cases, locationsToReadForDecode) over ErasureCode's default bulk loops;
-the product builds the same maps as matrices (hrs_api.cpp: src_encode_matrix,
+the product builds the same maps as matrices (hrs_matrix.cpp: src_encode_matrix,
 build_src_decode_matrix). The reference holds no SRC test or fixture, so the
 pin is the transcription plus the round-trip property over every erasure
 pattern (as for RS).
