@@ -1,5 +1,5 @@
-"""Encode-kernel timing for A/B runs of the static XOR network
-(HRS_ENC_SCHED=0|2|4|k): device-resident [S, n, L] hops-order stripes,
+"""Encode-kernel timing (round 2 used it for A/B builds of the static XOR
+network; it times whatever libhrs.so / HRS_LIB is loaded): device-resident [S, n, L] hops-order stripes,
 hrs_encode_dev on the current stream, HIP-event times, algorithmic bytes =
 (k + p) * L * S. Checks every variant's parity against a fixed reference
 digest of the first run in the same process (plane-by-plane vs factored
