@@ -69,6 +69,9 @@ def parse(argv=None):
     ap.add_argument("--check", action="store_true", help="verify a sample against the oracle after timing")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group even with one rank, so the collectives really run "
+                         "(one-GPU rehearsal of the RCCL calls)")
     ap.add_argument("--print-launch", action="store_true",
                     help="print the launch decision as JSON and exit (no GPU work; tests)")
     return ap.parse_args(argv)
@@ -104,7 +107,12 @@ def setup_dist(args):
     if args.dist_backend != "nccl":  # rehearsal: several ranks may share a GPU
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.force_dist:
+        if world == 1:  # single-rank group: a rendezvous of its own
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -302,7 +310,7 @@ def block_sha256(rows_of, S, g0, block=256):
 def gather_blocks(mine, world):
     """Union of every rank's block digests (all_gather_object)."""
     allv = [mine]
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():
         allv = [None] * world
         dist.all_gather_object(allv, mine)
     merged = {}
@@ -620,6 +628,7 @@ def run(args):
                             f"{S} stripes/GPU, device-resident",
                 "stripes_per_gpu": S, "stripes_total": total_stripes, "cell_bytes": L, "k": k, "p": p,
                 "parallelism": f"stripe-sharded x{world} (RCCL: matrix broadcast + barriers only)",
+                "collectives": (dist.get_backend() if dist.is_available() and dist.is_initialized() else None),
             },
             "parity_vs_oracle": vs_oracle,
             "encode_GiBps_per_gpu": round(k * L * S / GiB / (enc_ms * 1e-3), 3),
@@ -679,7 +688,7 @@ def run(args):
             res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 40, threads=1)
             res["cpu_baseline"]["gpu_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     return 0

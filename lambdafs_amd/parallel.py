@@ -12,12 +12,18 @@ import torch
 import torch.distributed as dist
 
 
+def active():
+    """A process group exists: every collective below goes through it, even
+    with one rank (bench.py --force-dist runs the RCCL calls on one GPU)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def world():
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    return dist.get_world_size() if active() else 1
 
 
 def rank():
-    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+    return dist.get_rank() if active() else 0
 
 
 def stripe_range(total, nranks, r):
@@ -31,11 +37,11 @@ def broadcast_matrix(m, device="cpu"):
     """Broadcast rank 0's uint8 coding matrix; raise if any rank's own differs."""
     m = np.ascontiguousarray(np.asarray(m, dtype=np.uint8))
     t = torch.from_numpy(m.copy()).to(device)
-    if world() > 1:
+    if active():
         dist.broadcast(t, src=0)
     got = t.cpu().numpy()
     same = torch.tensor([1 if np.array_equal(got, m) else 0], device=device)
-    if world() > 1:
+    if active():
         dist.all_reduce(same, op=dist.ReduceOp.MIN)
     if int(same.item()) != 1:
         raise RuntimeError("coding matrices differ across ranks")
@@ -43,12 +49,12 @@ def broadcast_matrix(m, device="cpu"):
 
 
 def barrier():
-    if world() > 1:
+    if active():
         dist.barrier()
 
 
 def max_over_ranks(x, device="cpu"):
-    if world() == 1:
+    if not active():
         return float(x)
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -56,7 +62,7 @@ def max_over_ranks(x, device="cpu"):
 
 
 def all_ok(flag, device="cpu"):
-    if world() == 1:
+    if not active():
         return bool(flag)
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)

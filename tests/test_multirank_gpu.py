@@ -57,3 +57,22 @@ def test_gpus_two_without_launcher_runs_two_ranks(cuda):
     assert one["parity_sha256"]["blocks"] == two["parity_sha256"]["blocks"]
     assert one["parity_sha256"]["decode_blocks"] == two["parity_sha256"]["decode_blocks"]
     assert two["parity_vs_oracle"] == {"blocks": 4, "match": True}
+
+
+def test_rccl_collectives_single_rank(cuda):
+    """The RCCL path on the box's one GPU: --force-dist creates an nccl
+    (= RCCL) process group with one rank bound to its device, so every
+    collective bench.py makes at N GPUs really runs through RCCL here — the
+    uint8 matrix broadcasts, the int64 MIN / float64 MAX / int32 MIN
+    all-reduces, the barriers, and all_gather_object of the digest blocks,
+    the config-5 leg included. (Two ranks cannot share one GPU under RCCL;
+    the N-rank curve is the driver's.)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--force-dist", "--dist-backend", "nccl",
+           "--stripes", "256", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["config"]["collectives"] == "nccl" and line["n_gpus"] == 1
+    assert line["parity_vs_oracle"] == {"blocks": 2, "match": True}
+    assert line["e2e_config5"]["bit_exact"] and line["e2e_config5"]["repaired_vs_oracle"] == {"blocks": 2, "match": True}
