@@ -4,6 +4,12 @@
  * tests/ as the parity checker and by bench.py as the timed CPU baseline
  * ("restated reference CPU path"); never by the product library.
  *
+ * Pinning: RS parity is "parity unpinned" in the strict sense — the reference
+ * is Java (no JDK here, so it cannot be run) and holds no RS golden vectors;
+ * this restatement is cross-checked by an independent Python transcription
+ * (rs_ref.py) and the reference's own property tests. The
+ * CRC-32 tables are pinned to the reference's CRC32_T8 tables.
+ *
  * Reference files (under /root/reference):
  *   GaloisField.java     hops-erasure-coding-project/hops-erasure-coding/src/main/java/io/hops/erasure_coding/
  *   ReedSolomonCode.java same directory
