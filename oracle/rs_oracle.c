@@ -416,6 +416,176 @@ void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int 
   }
 }
 
+/* ---------------------------- Apache Java RS coder (ported from ISA-L) */
+/* hadoop-common .../io/erasurecode/rawcoder/util/GF256.java. The literal
+ * tables GF_BASE (:35-88) and GF_LOG_BASE (:94-147) are regenerated here
+ * (powers of 2 mod 0x11D; the log table stores log(1) as 0xff and log(0) as
+ * 0) and pinned to the reference's numbers by tests/test_nrs_apache.py. */
+static uint8_t ap_base[256], ap_log[256];
+
+__attribute__((constructor)) static void ap_init(void) {
+  int v = 1;
+  for (int i = 0; i < 256; i++) {
+    ap_base[i] = (uint8_t)v;
+    v <<= 1;
+    if (v & 0x100) v ^= 0x11D;
+  }
+  ap_log[0] = 0;
+  for (int i = 0; i < 255; i++) ap_log[ap_base[i]] = (uint8_t)i;
+  ap_log[1] = 0xff; /* GF_LOG_BASE[1] */
+}
+
+int orc_apache_gf_base(int i) { return ap_base[i & 0xff]; }
+int orc_apache_gf_log_base(int i) { return ap_log[i & 0xff]; }
+
+/* GF256.gfMul, :172-184 */
+int orc_apache_gf_mul(int a, int b) {
+  if (a == 0 || b == 0) return 0;
+  int tmp = ap_log[a & 0xff] + ap_log[b & 0xff];
+  if (tmp > 254) tmp -= 255;
+  return ap_base[tmp];
+}
+
+/* GF256.gfInv, :186-192: GF_BASE[255 - GF_LOG_BASE[a] & 0xff] (Java: the
+ * subtraction binds first, then & 0xff). */
+int orc_apache_gf_inv(int a) {
+  if (a == 0) return 0;
+  return ap_base[(255 - ap_log[a & 0xff]) & 0xff];
+}
+
+/* GF256.gfInvertMatrix, :199-265 (throws "Not invertible": -1 here). */
+static int ap_invert(uint8_t* in, uint8_t* out, int n) {
+  for (int i = 0; i < n * n; i++) out[i] = 0;
+  for (int i = 0; i < n; i++) out[i * n + i] = 1;
+  for (int i = 0; i < n; i++) {
+    if (in[i * n + i] == 0) {
+      int j;
+      for (j = i + 1; j < n; j++)
+        if (in[j * n + i] != 0) break;
+      if (j == n) return -1;
+      for (int t = 0; t < n; t++) {
+        uint8_t x = in[i * n + t];
+        in[i * n + t] = in[j * n + t];
+        in[j * n + t] = x;
+        x = out[i * n + t];
+        out[i * n + t] = out[j * n + t];
+        out[j * n + t] = x;
+      }
+    }
+    const int temp = orc_apache_gf_inv(in[i * n + i]);
+    for (int j = 0; j < n; j++) {
+      in[i * n + j] = (uint8_t)orc_apache_gf_mul(in[i * n + j], temp);
+      out[i * n + j] = (uint8_t)orc_apache_gf_mul(out[i * n + j], temp);
+    }
+    for (int j = 0; j < n; j++) {
+      if (j == i) continue;
+      const int f = in[j * n + i];
+      for (int t = 0; t < n; t++) {
+        out[j * n + t] ^= (uint8_t)orc_apache_gf_mul(f, out[i * n + t]);
+        in[j * n + t] ^= (uint8_t)orc_apache_gf_mul(f, in[i * n + t]);
+      }
+    }
+  }
+  return 0;
+}
+
+/* GF256.gfVectMulInit, :267-337: the 32-byte multiply table of c (ISA-L's
+ * gf_vect_mul_init); RSUtil.encodeData reads its entry 1 (= c). */
+static void ap_vect_mul_init(uint8_t c, uint8_t* tbl) {
+#define AP_X2(v) ((uint8_t)(((v) << 1) ^ (((v)&0x80) ? 0x1d : 0)))
+  const uint8_t c2 = AP_X2(c), c4 = AP_X2(c2), c8 = AP_X2(c4);
+  const uint8_t c3 = c2 ^ c, c5 = c4 ^ c, c6 = c4 ^ c2, c7 = c4 ^ c3;
+  const uint8_t lo[16] = {0, c, c2, c3, c4, c5, c6, c7, c8, (uint8_t)(c8 ^ c), (uint8_t)(c8 ^ c2),
+                          (uint8_t)(c8 ^ c3), (uint8_t)(c8 ^ c4), (uint8_t)(c8 ^ c5), (uint8_t)(c8 ^ c6),
+                          (uint8_t)(c8 ^ c7)};
+  const uint8_t c17 = AP_X2(c8), c18 = AP_X2(c17), c19 = c18 ^ c17, c20 = AP_X2(c18);
+  const uint8_t c21 = c20 ^ c17, c22 = c20 ^ c18, c23 = c20 ^ c19, c24 = AP_X2(c20);
+  const uint8_t hi[16] = {0,   c17, c18, c19, c20, c21, c22, c23, c24, (uint8_t)(c24 ^ c17), (uint8_t)(c24 ^ c18),
+                          (uint8_t)(c24 ^ c19), (uint8_t)(c24 ^ c20), (uint8_t)(c24 ^ c21), (uint8_t)(c24 ^ c22),
+                          (uint8_t)(c24 ^ c23)};
+#undef AP_X2
+  memcpy(tbl, lo, 16);
+  memcpy(tbl + 16, hi, 16);
+}
+
+/* RSUtil.genCauchyMatrix, :63-76: identity on top, then a[i][j] = gfInv(i ^ j). */
+void orc_apache_gen_cauchy(uint8_t* a, int m, int k) {
+  memset(a, 0, (size_t)m * k);
+  for (int i = 0; i < k; i++) a[k * i + i] = 1;
+  int pos = k * k;
+  for (int i = k; i < m; i++)
+    for (int j = 0; j < k; j++) a[pos++] = (uint8_t)orc_apache_gf_inv(i ^ j);
+}
+
+/* RSUtil.initTables, :47-58, then RSUtil.encodeData(byte[]...), :86-135:
+ * outputs[l] ^= mul(coefficient (tables[j*32 + l*ninputs*32 + 1]), inputs[j])
+ * byte by byte; outputs are zeroed first (CoderUtil.resetOutputBuffers). */
+static void ap_encode_data(int ninputs, int noutputs, const uint8_t* coding_matrix, uint8_t* const* inputs,
+                           uint8_t* const* outputs, size_t len) {
+  uint8_t* tables = (uint8_t*)malloc((size_t)ninputs * noutputs * 32);
+  int offset = 0, idx = 0;
+  for (int i = 0; i < noutputs; i++)
+    for (int j = 0; j < ninputs; j++, offset += 32) ap_vect_mul_init(coding_matrix[idx++], tables + offset);
+  for (int l = 0; l < noutputs; l++) {
+    memset(outputs[l], 0, len);
+    for (int j = 0; j < ninputs; j++) {
+      const int s = tables[j * 32 + l * ninputs * 32 + 1];
+      for (size_t i = 0; i < len; i++) outputs[l][i] ^= (uint8_t)orc_apache_gf_mul(s, inputs[j][i]);
+    }
+  }
+  free(tables);
+}
+
+/* RSRawEncoder: constructor :45-60 (encodeMatrix = genCauchyMatrix(k + p, k),
+ * tables from its rows k..), doEncode(ByteArrayEncodingState) :71-78. */
+void orc_apache_rs_encode(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  uint8_t* a = (uint8_t*)malloc((size_t)(k + p) * k);
+  orc_apache_gen_cauchy(a, k + p, k);
+  ap_encode_data(k, p, a + (size_t)k * k, inputs, outputs, len);
+  free(a);
+}
+
+/* RSRawDecoder.doDecode(ByteArrayDecodingState), :87-102: validIndexes =
+ * the non-null inputs (CoderUtil.getValidIndexes), the first k of them read;
+ * processErasures :120-144 and generateDecodeMatrix :147-176. */
+int orc_apache_rs_decode(int k, int p, uint8_t* const* inputs, const int* erased, int ne, uint8_t* const* outputs,
+                         size_t len) {
+  const int n = k + p;
+  int valid[256], nvalid = 0;
+  for (int i = 0; i < n; i++)
+    if (inputs[i]) valid[nvalid++] = i;
+  if (nvalid < k) return -1;
+  uint8_t* enc = (uint8_t*)malloc((size_t)n * k);
+  orc_apache_gen_cauchy(enc, n, k);
+  int nerased_data = 0;
+  for (int i = 0; i < ne; i++)
+    if (erased[i] < k) nerased_data++;
+  uint8_t* tmp = (uint8_t*)calloc((size_t)n * k, 1);
+  uint8_t* inv = (uint8_t*)calloc((size_t)n * k, 1);
+  uint8_t* dec = (uint8_t*)calloc((size_t)n * k, 1);
+  for (int i = 0; i < k; i++)
+    for (int j = 0; j < k; j++) tmp[k * i + j] = enc[k * valid[i] + j];
+  int rc = ap_invert(tmp, inv, k);
+  if (rc == 0) {
+    for (int i = 0; i < nerased_data; i++)
+      for (int j = 0; j < k; j++) dec[k * i + j] = inv[k * erased[i] + j];
+    for (int q = nerased_data; q < ne; q++)
+      for (int i = 0; i < k; i++) {
+        uint8_t s = 0;
+        for (int j = 0; j < k; j++) s ^= (uint8_t)orc_apache_gf_mul(inv[j * k + i], enc[k * erased[q] + j]);
+        dec[k * q + i] = s;
+      }
+    uint8_t* real[256];
+    for (int i = 0; i < k; i++) real[i] = inputs[valid[i]];
+    ap_encode_data(k, ne, dec, real, outputs, len);
+  }
+  free(enc);
+  free(tmp);
+  free(inv);
+  free(dec);
+  return rc;
+}
+
 /* ------------------------------------------------- nrs (ISA-L Cauchy RS) */
 
 /* ISA-L gf_mul / gf_inv over 0x11D: the same field as GaloisField (285). */

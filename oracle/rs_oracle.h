@@ -80,12 +80,31 @@ void orc_xor_decode_bulk(int k, uint8_t* const* read_bufs, uint8_t* output, int 
 /* NativeReedSolomonCode (the `nrs` codec, hops-erasure-coding/.../NativeReedSolomonCode.java)
  * over libhadoop's ISA-L shim (hadoop-common/src/main/native/src/org/apache/hadoop/io/
  * erasurecode/erasure_coder.c) and ISA-L (absent here, version unpinned: restated from its
- * published gf_gen_cauchy1_matrix / gf_invert_matrix / ec_encode_data definitions).
+ * published gf_gen_cauchy1_matrix / gf_invert_matrix / ec_encode_data definitions; checked
+ * against orc_apache_* below, the restated Java port of ISA-L the reference itself ships).
  * Rows in hops order [parity, data]; read_bufs entries may be NULL (not read). */
 void orc_nrs_encode_matrix(int k, int p, uint8_t* a /* (k+p) x k, ISA-L layout */);
 void orc_nrs_encode_bulk(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len);
 int orc_nrs_decode_bulk(int k, int p, uint8_t* const* read_bufs, uint8_t* const* write_bufs, const int* erased,
                         int ne, const int* not_to_read, int nn, size_t len);
+
+/* The reference's pure-Java port of ISA-L's RS coder (hadoop-common/src/main/java/org/apache/
+ * hadoop/io/erasurecode/rawcoder/: RSRawEncoder.java, RSRawDecoder.java, util/RSUtil.java,
+ * util/GF256.java), restated loop for loop. The reference's own interop tests
+ * (TestRSRawCoderInteroperable1/2: Java encode + native decode and the reverse) hold it equal to
+ * the native ISA-L coder behind the `nrs` codec, so it pins orc_nrs_* to reference source.
+ * Apache unit order [data 0..k-1, parity k..k+p-1]. */
+int orc_apache_gf_base(int i);      /* GF256.GF_BASE[i], regenerated; tests pin it to the literal */
+int orc_apache_gf_log_base(int i);  /* GF256.GF_LOG_BASE[i] (log(1) stored as 0xff) */
+int orc_apache_gf_mul(int a, int b);
+int orc_apache_gf_inv(int a);
+void orc_apache_gen_cauchy(uint8_t* a, int m, int k);  /* RSUtil.genCauchyMatrix, m x k */
+void orc_apache_rs_encode(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len);
+/* RSRawDecoder.doDecode(ByteArrayDecodingState): inputs[k + p] with NULL for units not read
+ * (erased included), erased = the erased unit indexes (ascending, as the hops wrapper passes
+ * them), outputs[ne]. Returns 0, or -1 if fewer than k inputs or the matrix is singular. */
+int orc_apache_rs_decode(int k, int p, uint8_t* const* inputs, const int* erased, int ne, uint8_t* const* outputs,
+                         size_t len);
 
 /* SimpleRegeneratingCode (the `src` codec, SimpleRegeneratingCode.java:28-482),
  * with ErasureCode's default bulk loops (ErasureCode.java:136-181). s_in is

@@ -66,6 +66,13 @@ def lib():
             "orc_nrs_encode_matrix": ([I, I, ctypes.c_void_p], None),
             "orc_nrs_encode_bulk": ([I, I, PP, PP, S], None),
             "orc_nrs_decode_bulk": ([I, I, PP, PP, IP, I, IP, I, S], I),
+            "orc_apache_gf_base": ([I], I),
+            "orc_apache_gf_log_base": ([I], I),
+            "orc_apache_gf_mul": ([I, I], I),
+            "orc_apache_gf_inv": ([I], I),
+            "orc_apache_gen_cauchy": ([ctypes.c_void_p, I, I], None),
+            "orc_apache_rs_encode": ([I, I, PP, PP, S], None),
+            "orc_apache_rs_decode": ([I, I, PP, IP, I, PP, S], I),
             "orc_src_params": ([I, I, I, IP, IP, IP], I),
             "orc_src_encode": ([I, I, I, IP, IP], None),
             "orc_src_decode5": ([I, I, I, IP, IP, I, IP, IP, I, IP, I], I),
@@ -271,6 +278,56 @@ def nrs_decode_bulk(k, p, read_bufs, erased, not_to_read):
                                    _ints(not_to_read), len(not_to_read), L)
     assert st == 0
     return outs
+
+
+# ------------------------- Apache Java RS coder (RSRawEncoder / RSRawDecoder)
+
+def apache_gen_cauchy(m, k):
+    a = np.zeros((m, k), dtype=np.uint8)
+    lib().orc_apache_gen_cauchy(a.ctypes.data, m, k)
+    return a
+
+
+def apache_rs_encode(k, p, inputs):
+    """RSRawEncoder.encode: k data units -> p parity units (Apache order)."""
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    outs = [np.zeros(rows[0].size, dtype=np.uint8) for _ in range(p)]
+    lib().orc_apache_rs_encode(k, p, _rowptrs(rows), _rowptrs(outs), rows[0].size)
+    return outs
+
+
+def apache_rs_decode(k, p, inputs, erased):
+    """RSRawDecoder.decode: inputs[k + p] in Apache order (None = not read),
+    erased unit indexes (ascending) -> their values."""
+    rows = [None if r is None else np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    L = max(r.size for r in rows if r is not None)
+    outs = [np.zeros(L, dtype=np.uint8) for _ in erased]
+    st = lib().orc_apache_rs_decode(k, p, _rowptrs(rows), _ints(erased), len(erased), _rowptrs(outs), L)
+    assert st == 0, "RSRawDecoder: fewer than k inputs or singular"
+    return outs
+
+
+def hops_nrs_decode_via_apache(k, p, read_bufs, erased, not_to_read):
+    """NativeReedSolomonCode.decodeBulk (NativeReedSolomonCode.java:90-148)
+    with the reference's pure-Java RSRawDecoder in place of the native one it
+    is interoperable with: hops rows [parity, data] -> Apache units [data,
+    parity], the not-to-read units nulled and their sorted Apache indexes
+    decoded, the first len(erased) outputs returned (the Java copies
+    bwriteBufs[i] into writeBufs[i] for i < writeBufs.length)."""
+    n = k + p
+    units = [None] * n
+    for i in range(p):
+        units[i + k] = read_bufs[i]
+    for i in range(k):
+        units[i] = read_bufs[i + p]
+    mod = []
+    for loc in not_to_read:
+        a = loc + k if loc < p else loc - p
+        units[a] = None
+        mod.append(a)
+    mod.sort()
+    outs = apache_rs_decode(k, p, units, mod)
+    return outs[:len(erased)]
 
 
 # ------------------------------------------- SimpleRegeneratingCode (src)

@@ -1,4 +1,5 @@
-// Dumps, as JSON, the CRC-32 tables the engine's kernels use, for
+// Dumps, as JSON, the CRC-32 and GF(2^8) tables the engine uses, for
+// tests/test_nrs_apache.py (GF tables vs the reference's GF256 literals) and
 // tests/test_crc_tables.py to compare with the reference's own tables
 // (tests/golden/crc32_tables.json <- hadoop-common's
 // crc32_zlib_polynomial_tables.h): the slicing tables as laid out in the
@@ -9,6 +10,7 @@
 #include <cstdio>
 #include <vector>
 
+#include "../../lambdafs_amd/csrc/gf256.hpp"
 #include "../../lambdafs_amd/csrc/hrs_crc.hpp"
 
 namespace cr = hrs::crc;
@@ -44,6 +46,14 @@ int main() {
     char name[32];
     std::snprintf(name, sizeof name, "zeros_T8_%d", j);
     dump(name, t, 256);
+  }
+  {  // the engine's GF(2^8) tables (gf256.hpp: host matrices, byte-granular kernels)
+    const hrs::gf::Tables g = hrs::gf::make_tables();
+    uint32_t e[512], l[256];
+    for (int i = 0; i < 512; ++i) e[i] = g.exp[i];
+    for (int i = 0; i < 256; ++i) l[i] = g.log[i];
+    dump("gf_exp", e, 512);
+    dump("gf_log", l, 256);
   }
   dump("lds_z_chunk", &img[hrs::kCrcSliceWords], 1024);
   dump("lds_z_tree", &img[hrs::kCrcSliceWords + 1024], 6 * 1024, true);
