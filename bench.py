@@ -344,23 +344,31 @@ def compare_blocks(got, want, fields):
     return {"blocks": n, "match": True} if n else None
 
 
-def hbm_probes(dev, nbytes=4 << 30, reps=5):
+def hbm_probes(dev, stripes=None, patterns=(), nbytes=4 << 30, reps=5):
     """This GPU's streaming ceilings, measured in this run by the engine's
-    probes (include/hrs_probe.h: nontemporal 16-byte grid-stride kernels,
-    256-thread blocks), median of `reps` over 4 GiB buffers:
-      copy  : read + write of 4 GiB (hrs_probe_copy at 2 and 4 blocks per CU,
-              and torch's D2D copy_) — SURVEY §8d's "device-copy STREAM peak";
-      read  : read-only stream (hrs_probe_read, 4 blocks per CU);
-      write : write-only stream (hrs_probe_write, 4 blocks per CU).
-    A 1:1 copy is not a ceiling for the codec's read-heavy mixes (10 reads per
-    4 writes for RS(10,4) encode, per 1 write for a repair): reads and writes
-    share HBM's data bus, so the ceiling of a mix of R bytes read and W
-    written is (R + W) / (R / read + W / write) (mix_ceiling)."""
+    probes (include/hrs_probe.h), median of `reps` launches each; every
+    figure is the fastest of a small sweep of shapes (wave-task chunk of 1 or
+    8 contiguous KiB, nontemporal or default policy, 1/2/4 blocks of 256
+    threads per CU; round 1's lab found the best shape differs per stream,
+    profiles/r01/lab8_bw_ceilings.txt):
+      copy    : 4 GiB read + 4 GiB written (hrs_probe_stream COPY, and
+                torch's D2D copy_) — SURVEY §8d's "device-copy STREAM peak";
+      read    : read-only stream of 4 GiB;
+      write   : write-only stream of 4 GiB;
+      pattern : for each (name, nread, nwrite) in `patterns`, the coding
+                kernels' access pattern without the math (hrs_probe_rows) over
+                `stripes` [S, n, L] itself — same buffer, same bytes, same
+                2 KiB-window order. This is the ceiling of the pattern: a 1:1
+                copy is not one for the codec's read-heavy mixes, and the mix
+                of the read-only and write-only peaks ((R + W) / (R / read +
+                W / write), mix_ceiling) is optimistic, because HBM pays for
+                turning its bus between reads and writes.
+    The pattern probe overwrites rows [0, nwrite) of every stripe: call it
+    after the stripes' outputs have been checked."""
     src = torch.empty((nbytes >> 20, 1 << 20), dtype=torch.uint8, device=dev)
     src.fill_(0x5A)
     dst = torch.empty_like(src)
     sink = torch.zeros(4096, dtype=torch.uint8, device=dev)
-    out = {}
 
     def timed(fn):
         fn()
@@ -374,34 +382,65 @@ def hbm_probes(dev, nbytes=4 << 30, reps=5):
             times.append(a.elapsed_time(b))
         return float(np.median(times))
 
-    for name, fn in (("probe_nt_4cu", lambda: device.probe_copy(src, dst, 4)),
-                     ("probe_nt_2cu", lambda: device.probe_copy(src, dst, 2)),
-                     ("torch_copy", lambda: dst.copy_(src))):
-        out[name] = round(2 * nbytes / (timed(fn) * 1e-3) / 1e9, 1)
+    def rate(moved, fn):
+        return round(moved / (timed(fn) * 1e-3) / 1e9, 1)
+
+    shapes = [(c, nt, bpc) for c in (1, 8) for nt in (True, False) for bpc in (1, 2, 4)]
+    tag = lambda c, nt, bpc: f"{c}K_{'nt' if nt else 'plain'}_{bpc}cu"
+    copies = {}
+    for c, nt, bpc in shapes:
+        copies[tag(c, nt, bpc)] = rate(2 * nbytes, lambda: device.probe_copy(src, dst, bpc, c, nt))
         if not torch.equal(dst[::97], src[::97]):
-            raise RuntimeError(f"copy probe {name} mismatch")
+            raise RuntimeError(f"copy probe {tag(c, nt, bpc)} mismatch")
         dst.zero_()
-    read = round(nbytes / (timed(lambda: device.probe_read(src, sink, 4)) * 1e-3) / 1e9, 1)
-    write = round(nbytes / (timed(lambda: device.probe_write(dst, 4)) * 1e-3) / 1e9, 1)
-    if int(sink.sum().item()) != 0 or dst[0, 4:8].tolist() != [0x5A] * 4:  # element 0 = (0, 0x5A5A5A5A, ..)
+    copies["torch_copy"] = rate(2 * nbytes, lambda: dst.copy_(src))
+    reads = {tag(c, True, bpc): rate(nbytes, lambda: device.probe_read(src, sink, bpc, c, True))
+             for c in (1, 8) for bpc in (1, 2, 4)}
+    writes = {tag(c, nt, bpc): rate(nbytes, lambda: device.probe_write(dst, bpc, c, nt)) for c, nt, bpc in shapes}
+    if int(sink.sum().item()) != 0 or dst[0, 4:8].tolist() != [0x5A] * 4:  # element 0 = (t, 0x5A5A5A5A, ..)
         raise RuntimeError("read / write probes did not run as intended")
     del src, dst, sink
     torch.cuda.empty_cache()
-    copy = max(out["probe_nt_4cu"], out["probe_nt_2cu"], out["torch_copy"])
-    return {
-        "copy": {**out, "GBps": copy,
-                 "how": "4 GiB D2D, median of 5: hrs_probe_copy (nontemporal float4 grid-stride copy, 256-thread "
-                        "blocks, 2 and 4 per CU) and torch copy_; GBps = the fastest"},
-        "read_GBps": read,
-        "write_GBps": write,
-        "how": "hrs_probe_read / hrs_probe_write over 4 GiB, 4 blocks per CU, median of 5",
+    best = lambda d: max(d, key=d.get)
+    out = {
+        "copy": {"GBps": copies[best(copies)], "best": best(copies), "variants": copies,
+                 "how": "4 GiB D2D (bytes read + written), hrs_probe_stream COPY over the shape sweep and torch "
+                        "copy_; GBps = the fastest"},
+        "read_GBps": reads[best(reads)], "read_best": best(reads),
+        "write_GBps": writes[best(writes)], "write_best": best(writes),
+        "read_variants": reads, "write_variants": writes,
+        "how": "hrs_probe_stream READ / WRITE over 4 GiB, fastest of the shape sweep (task chunk KiB, policy, "
+               "blocks per CU), median of 5 launches each",
+        "pattern": {},
     }
+    if stripes is not None:
+        S, n, L = stripes.shape
+        for name, nr, nw in patterns:
+            moved = (nr + nw) * L * S
+            try:
+                v = {f"{bpc}cu": rate(moved, lambda: device.probe_rows(stripes, nr, nw, bpc)) for bpc in (1, 2, 4)}
+            except Exception as e:  # a (nread, nwrite) pair hrs_probe_rows does not instantiate
+                out["pattern"][name] = {"error": str(e)}
+                continue
+            out["pattern"][name] = {"GBps": v[best(v)], "best": best(v), "variants": v, "reads": nr, "writes": nw,
+                                    "how": f"hrs_probe_rows over the bench's own {S} x {n} x {L} stripes: "
+                                           f"{nr} rows read / {nw} written per 2 KiB window, no math"}
+    return out
 
 
 def mix_ceiling(probes, rbytes, wbytes):
     """Ceiling of a stream of rbytes read and wbytes written on this GPU:
     reads and writes share the HBM data bus, each at its own measured peak."""
     return (rbytes + wbytes) / (rbytes / probes["read_GBps"] + wbytes / probes["write_GBps"])
+
+
+def pattern_fields(probes, name, gbps):
+    """roofline.pattern_ceiling / frac_vs_pattern: the kernel against the
+    no-math probe of its own access pattern (hbm_probes "pattern")."""
+    pat = probes["pattern"].get(name, {})
+    if "GBps" not in pat:
+        return {"pattern_ceiling": None, "frac_vs_pattern": None}
+    return {"pattern_ceiling": pat["GBps"], "frac_vs_pattern": round(gbps / pat["GBps"], 4)}
 
 
 def stats(ms):
@@ -605,7 +644,8 @@ def run(args):
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
     res = None
-    probes = hbm_probes(dev) if rank == 0 else None
+    # after the digests: the pattern probe overwrites parity rows of `stripes`
+    probes = (hbm_probes(dev, stripes, (("encode", k, p), ("decode", k, len(erased)))) if rank == 0 else None)
     if rank == 0:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             traffic_note = json.load(f).get("_note")
@@ -649,6 +689,7 @@ def run(args):
                 "frac_vs_copy": round(enc_gbps / probes["copy"]["GBps"], 4),
                 "mix_ceiling": round(mix_ceiling(probes, k, p), 1),
                 "frac_vs_mix_ceiling": round(enc_gbps / mix_ceiling(probes, k, p), 4),
+                **pattern_fields(probes, "encode", enc_gbps),
             },
             "decode_roofline": {
                 "kernel": traffic_key(dec_kernel), "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
@@ -656,6 +697,7 @@ def run(args):
                 "launch_ms": stats(dec_all), "frac_vs_copy": round(dec_gbps / probes["copy"]["GBps"], 4),
                 "mix_ceiling": round(mix_ceiling(probes, k, len(erased)), 1),
                 "frac_vs_mix_ceiling": round(dec_gbps / mix_ceiling(probes, k, len(erased)), 4),
+                **pattern_fields(probes, "decode", dec_gbps),
                 "traffic": load_traffic(dec_kernel),
                 "algorithmic_bytes_per_launch": dec_bytes,
             },

@@ -39,6 +39,7 @@ EXPORTS = (
     "hrs_encode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
     "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_probe_copy", "hrs_probe_read", "hrs_probe_write", "hrs_wait",
+    "hrs_probe_stream", "hrs_probe_rows",
 )
 
 
@@ -110,6 +111,8 @@ def lib():
         "hrs_probe_copy": ([P, P, S, I, P], I),
         "hrs_probe_read": ([P, S, I, P, P], I),
         "hrs_probe_write": ([P, S, I, P], I),
+        "hrs_probe_stream": ([I, P, P, S, I, I, I, P], I),
+        "hrs_probe_rows": ([P, S, I, S, I, I, I, P], I),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -1,6 +1,14 @@
-// HBM ceiling probe (include/hrs_probe.h): the nontemporal 16-byte
-// grid-stride copy of tools/copy_probe.hip, built into libhrs so bench.py
-// measures its own copy ceiling beside the coding kernels in the same run.
+// HBM ceiling probes (include/hrs_probe.h), built into libhrs so bench.py
+// measures its own ceilings beside the coding kernels in the same run:
+//   - streams (copy / read-only / write-only) in the shape of round 1's
+//     bandwidth lab (tools/bw_lab.hip, profiles/r01/lab8_bw_ceilings.txt): a
+//     wave task is `chunk` KiB contiguous, one 16-byte access per lane per
+//     KiB, all of the task's loads issued before any is consumed;
+//   - the coding kernels' own access pattern with the math taken out
+//     (hrs_probe_rows): 2 KiB column windows of `nread` rows of a stripe-major
+//     [S][nrows][L] buffer read, `nwrite` rows written, nontemporal 16-byte
+//     accesses, one wave task per window, as encode_static_kernel and the
+//     pipelined repair kernel walk them.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -12,67 +20,182 @@
 namespace hrs {
 namespace {
 
-__global__ void __launch_bounds__(256) stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                           uint64_t n) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  return *p;
 }
 
-// Read-only stream: every 16-byte element loaded once (nontemporal); a lane
-// stores its XOR only if it equals an impossible value, so the loads stay.
-__global__ void __launch_bounds__(256) stream_read_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ sink,
-                                                           uint64_t n) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+template <bool NT>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// Elements [tail0, n) that do not fill a whole chunk: one 16-byte element per
+// thread of the grid (the chunked loop has covered [0, tail0)).
+__device__ __forceinline__ uint64_t tail_index() {
+  return static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+}
+
+// Stream ops: 0 copy, 1 read-only (XOR kept alive by an impossible store to
+// `sink`), 2 write-only. A task is C KiB = 64 * C elements of 16 bytes.
+template <int OP, int C, bool NT>
+__global__ void __launch_bounds__(256) stream_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                      uint64_t n) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t ntasks = n / (64u * C);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
   u32x4 acc = {0u, 0u, 0u, 0u};
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-    acc ^= __builtin_nontemporal_load(&src[i]);
-  if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9E3779B9u && acc[0] == 0x7F4A7C15u) sink[threadIdx.x] = acc;
+  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nw) {
+    const uint64_t e = t * 64u * C + lane;
+    if constexpr (OP == 2) {
+      const uint32_t v = static_cast<uint32_t>(t);
+#pragma unroll
+      for (int j = 0; j < C; ++j) st16<NT>(&dst[e + 64u * j], u32x4{v, 0x5A5A5A5Au, ~v, static_cast<uint32_t>(j)});
+    } else {
+      u32x4 v[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) v[j] = ld16<NT>(&src[e + 64u * j]);
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if constexpr (OP == 0) st16<NT>(&dst[e + 64u * j], v[j]);
+        else acc ^= v[j];
+      }
+    }
+  }
+  const uint64_t i = ntasks * 64u * C + tail_index();
+  if (i < n) {
+    if constexpr (OP == 0) dst[i] = src[i];
+    else if constexpr (OP == 1) acc ^= src[i];
+    else dst[i] = u32x4{0u, 0x5A5A5A5Au, ~0u, 0u};
+  }
+  if constexpr (OP == 1)
+    if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9E3779B9u && acc[0] == 0x7F4A7C15u) dst[threadIdx.x] = acc;
 }
 
-// Write-only stream: every 16-byte element stored once (nontemporal).
-__global__ void __launch_bounds__(256) stream_write_kernel(u32x4* __restrict__ dst, uint64_t n) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t v = static_cast<uint32_t>(i);
-    __builtin_nontemporal_store(u32x4{v, v ^ 0x5A5A5A5Au, ~v, v * 0x9E3779B9u}, &dst[i]);
+// The codec's access pattern without the math: task t = (stripe, 2 KiB window);
+// read rows [nrows - R, nrows), write rows [0, W) with the XOR of the reads
+// (+ the row index), every access nontemporal, all R rows' loads issued first.
+template <int R, int W>
+__global__ void __launch_bounds__(256) rows_kernel(uint8_t* __restrict__ base, uint64_t nstripes, int nrows,
+                                                    uint64_t L) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwin = L / 2048u;
+  const uint64_t ntasks = nstripes * nwin;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nw) {
+    const uint64_t s = t / nwin;
+    uint8_t* sb = base + s * nrows * L + (t - s * nwin) * 2048u + lane * 16;
+    u32x4 v[R][2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(sb + (nrows - R + r) * L);
+      v[r][0] = __builtin_nontemporal_load(p);
+      v[r][1] = __builtin_nontemporal_load(p + 64);
+    }
+    u32x4 a = v[0][0], b = v[0][1];
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      a ^= v[r][0];
+      b ^= v[r][1];
+    }
+#pragma unroll
+    for (int o = 0; o < W; ++o) {
+      u32x4* q = reinterpret_cast<u32x4*>(sb + o * L);
+      __builtin_nontemporal_store(a + static_cast<uint32_t>(o), q);
+      __builtin_nontemporal_store(b + static_cast<uint32_t>(o), q + 64);
+    }
   }
+}
+
+template <int OP, int C>
+hrs_status launch_stream_c(const void* src, void* dst, uint64_t n, bool nt, unsigned grid, hipStream_t st) {
+  const char* names[3] = {"stream_copy_kernel", "stream_read_kernel", "stream_write_kernel"};
+  note_kernel_t(names[OP], C, nt);
+  auto k = nt ? stream_kernel<OP, C, true> : stream_kernel<OP, C, false>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), n);
+  return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
+}
+
+template <int OP>
+hrs_status launch_stream(const void* src, void* dst, size_t bytes, int chunk_kib, int nt, int bpc, void* stream) {
+  const unsigned grid = static_cast<unsigned>(bpc * device_cus());
+  const uint64_t n = bytes / 16;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (chunk_kib) {
+    case 1: return launch_stream_c<OP, 1>(src, dst, n, nt != 0, grid, st);
+    case 2: return launch_stream_c<OP, 2>(src, dst, n, nt != 0, grid, st);
+    case 4: return launch_stream_c<OP, 4>(src, dst, n, nt != 0, grid, st);
+    case 8: return launch_stream_c<OP, 8>(src, dst, n, nt != 0, grid, st);
+    default: return HRS_EINVAL;
+  }
+}
+
+template <int R, int W>
+hrs_status launch_rows_rw(void* base, size_t nstripes, int nrows, size_t L, unsigned grid, hipStream_t st) {
+  note_kernel_t("probe_rows_kernel", R, W);
+  auto k = rows_kernel<R, W>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<uint8_t*>(base), static_cast<uint64_t>(nstripes),
+                     nrows, static_cast<uint64_t>(L));
+  return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
+}
+
+bool stream_args_ok(int chunk_kib, int bpc) {
+  return bpc >= 1 && bpc <= 32 && (chunk_kib == 1 || chunk_kib == 2 || chunk_kib == 4 || chunk_kib == 8);
 }
 
 }  // namespace
 }  // namespace hrs
 
-extern "C" hrs_status hrs_probe_copy(const void* src, void* dst, size_t bytes, int blocks_per_cu, void* stream) {
-  if (blocks_per_cu < 1 || blocks_per_cu > 32 || (bytes && (!src || !dst))) return HRS_EINVAL;
+extern "C" hrs_status hrs_probe_stream(int op, const void* src, void* dst, size_t bytes, int chunk_kib,
+                                       int nontemporal, int blocks_per_cu, void* stream) {
+  if (op < HRS_PROBE_COPY || op > HRS_PROBE_WRITE || !hrs::stream_args_ok(chunk_kib, blocks_per_cu)) return HRS_EINVAL;
+  const bool need_src = op != HRS_PROBE_WRITE;
+  if (bytes && ((need_src && !src) || !dst)) return HRS_EINVAL;
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) return HRS_EALIGN;
   if (bytes == 0) return HRS_OK;
-  const unsigned grid = static_cast<unsigned>(blocks_per_cu * hrs::device_cus());
-  hrs::note_kernel("stream_copy_kernel");
-  hipLaunchKernelGGL(hrs::stream_copy_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const hrs::u32x4*>(src), static_cast<hrs::u32x4*>(dst),
-                     static_cast<uint64_t>(bytes / 16));
-  return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
+  switch (op) {
+    case HRS_PROBE_COPY: return hrs::launch_stream<0>(src, dst, bytes, chunk_kib, nontemporal, blocks_per_cu, stream);
+    case HRS_PROBE_READ: return hrs::launch_stream<1>(src, dst, bytes, chunk_kib, nontemporal, blocks_per_cu, stream);
+    default: return hrs::launch_stream<2>(nullptr, dst, bytes, chunk_kib, nontemporal, blocks_per_cu, stream);
+  }
+}
+
+extern "C" hrs_status hrs_probe_copy(const void* src, void* dst, size_t bytes, int blocks_per_cu, void* stream) {
+  return hrs_probe_stream(HRS_PROBE_COPY, src, dst, bytes, 1, 1, blocks_per_cu, stream);
 }
 
 extern "C" hrs_status hrs_probe_read(const void* src, size_t bytes, int blocks_per_cu, void* sink, void* stream) {
-  if (blocks_per_cu < 1 || blocks_per_cu > 32 || !sink || (bytes && !src)) return HRS_EINVAL;
-  if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(sink) | bytes) & 15u) return HRS_EALIGN;
-  if (bytes == 0) return HRS_OK;
-  const unsigned grid = static_cast<unsigned>(blocks_per_cu * hrs::device_cus());
-  hrs::note_kernel("stream_read_kernel");
-  hipLaunchKernelGGL(hrs::stream_read_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const hrs::u32x4*>(src), static_cast<hrs::u32x4*>(sink),
-                     static_cast<uint64_t>(bytes / 16));
-  return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
+  if (!sink) return HRS_EINVAL;
+  return hrs_probe_stream(HRS_PROBE_READ, src, sink, bytes, 1, 1, blocks_per_cu, stream);
 }
 
 extern "C" hrs_status hrs_probe_write(void* dst, size_t bytes, int blocks_per_cu, void* stream) {
-  if (blocks_per_cu < 1 || blocks_per_cu > 32 || (bytes && !dst)) return HRS_EINVAL;
-  if ((reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) return HRS_EALIGN;
-  if (bytes == 0) return HRS_OK;
+  return hrs_probe_stream(HRS_PROBE_WRITE, nullptr, dst, bytes, 1, 1, blocks_per_cu, stream);
+}
+
+extern "C" hrs_status hrs_probe_rows(void* base, size_t nstripes, int nrows, size_t cell_bytes, int nread,
+                                     int nwrite, int blocks_per_cu, void* stream) {
+  if (blocks_per_cu < 1 || blocks_per_cu > 32 || nrows < 1 || nread < 1 || nwrite < 0 || nread + nwrite > nrows)
+    return HRS_EINVAL;
+  if (nstripes && !base) return HRS_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(base) & 15u) || (cell_bytes % 2048u)) return HRS_EALIGN;
+  if (nstripes == 0 || cell_bytes == 0) return HRS_OK;
   const unsigned grid = static_cast<unsigned>(blocks_per_cu * hrs::device_cus());
-  hrs::note_kernel("stream_write_kernel");
-  hipLaunchKernelGGL(hrs::stream_write_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<hrs::u32x4*>(dst), static_cast<uint64_t>(bytes / 16));
-  return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  // The read / write counts of the shapes bench.py and the tests quote:
+  // RS(10,4) encode and 1..4-erasure repairs, RS(6,3), RS(12,4), RS(3,2).
+  switch (nread * 100 + nwrite) {
+    case 1004: return hrs::launch_rows_rw<10, 4>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1003: return hrs::launch_rows_rw<10, 3>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1002: return hrs::launch_rows_rw<10, 2>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1001: return hrs::launch_rows_rw<10, 1>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1000: return hrs::launch_rows_rw<10, 0>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 603: return hrs::launch_rows_rw<6, 3>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1204: return hrs::launch_rows_rw<12, 4>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1202: return hrs::launch_rows_rw<12, 2>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 302: return hrs::launch_rows_rw<3, 2>(base, nstripes, nrows, cell_bytes, grid, st);
+    default: return HRS_EINVAL;
+  }
 }

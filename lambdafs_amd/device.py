@@ -195,32 +195,52 @@ def crc32_rows(code, row_views, crc_in=None):
     return out
 
 
-def probe_copy(src, dst, blocks_per_cu=4):
-    """HBM ceiling probe (include/hrs_probe.h): dst <- src, both contiguous
-    device tensors of the same byte size, by the nontemporal 16-byte
-    grid-stride copy kernel at `blocks_per_cu` blocks per CU, on the
-    current stream. Diagnostic: bench.py's copy_peak."""
-    nbytes = src.numel() * src.element_size()
+PROBE_COPY, PROBE_READ, PROBE_WRITE = 0, 1, 2
+
+
+def _nbytes(t):
+    return t.numel() * t.element_size()
+
+
+def probe_copy(src, dst, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
+    """HBM ceiling probe (include/hrs_probe.h, hrs_probe_stream): dst <- src,
+    both contiguous device tensors of the same byte size; wave tasks of
+    `chunk_kib` contiguous KiB at `blocks_per_cu` 256-thread blocks per CU,
+    on the current stream. Diagnostic: bench.py's copy_peak."""
     if (not src.is_cuda or not dst.is_cuda or not src.is_contiguous() or not dst.is_contiguous()
-            or dst.numel() * dst.element_size() != nbytes):
+            or _nbytes(dst) != _nbytes(src)):
         raise ValueError("probe_copy needs two contiguous device tensors of equal size")
-    st = _lib.lib().hrs_probe_copy(src.data_ptr(), dst.data_ptr(), nbytes, int(blocks_per_cu), _stream(src))
-    _lib.check(st)
+    _lib.check(_lib.lib().hrs_probe_stream(PROBE_COPY, src.data_ptr(), dst.data_ptr(), _nbytes(src), int(chunk_kib),
+                                           int(bool(nontemporal)), int(blocks_per_cu), _stream(src)))
 
 
-def probe_read(src, sink, blocks_per_cu=4):
-    """HBM read-only probe (hrs_probe_read): reads the contiguous device
-    tensor `src` once; `sink` is a device tensor of >= 4 KiB (never written
-    in practice)."""
-    if not src.is_cuda or not src.is_contiguous() or sink.numel() * sink.element_size() < 4096:
+def probe_read(src, sink, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
+    """HBM read-only probe (hrs_probe_stream READ): reads the contiguous
+    device tensor `src` once; `sink` is a device tensor of >= 4 KiB (never
+    written in practice)."""
+    if not src.is_cuda or not src.is_contiguous() or not sink.is_cuda or _nbytes(sink) < 4096:
         raise ValueError("probe_read needs a contiguous device tensor and a 4 KiB device sink")
-    _lib.check(_lib.lib().hrs_probe_read(src.data_ptr(), src.numel() * src.element_size(), int(blocks_per_cu),
-                                         sink.data_ptr(), _stream(src)))
+    _lib.check(_lib.lib().hrs_probe_stream(PROBE_READ, src.data_ptr(), sink.data_ptr(), _nbytes(src), int(chunk_kib),
+                                           int(bool(nontemporal)), int(blocks_per_cu), _stream(src)))
 
 
-def probe_write(dst, blocks_per_cu=4):
-    """HBM write-only probe (hrs_probe_write): writes the contiguous device tensor `dst` once."""
+def probe_write(dst, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
+    """HBM write-only probe (hrs_probe_stream WRITE): writes the contiguous
+    device tensor `dst` once."""
     if not dst.is_cuda or not dst.is_contiguous():
         raise ValueError("probe_write needs a contiguous device tensor")
-    _lib.check(_lib.lib().hrs_probe_write(dst.data_ptr(), dst.numel() * dst.element_size(), int(blocks_per_cu),
-                                          _stream(dst)))
+    _lib.check(_lib.lib().hrs_probe_stream(PROBE_WRITE, None, dst.data_ptr(), _nbytes(dst), int(chunk_kib),
+                                           int(bool(nontemporal)), int(blocks_per_cu), _stream(dst)))
+
+
+def probe_rows(stripes, nread, nwrite, blocks_per_cu=2):
+    """The coding kernels' access pattern without the math (hrs_probe_rows):
+    `stripes` is a contiguous uint8 device tensor [S, nrows, L]; per 2 KiB
+    column window rows [nrows - nread, nrows) are read and rows [0, nwrite)
+    overwritten with their XOR (+ the row index)."""
+    if (not stripes.is_cuda or stripes.dtype != _lib.torch.uint8 or stripes.dim() != 3
+            or not stripes.is_contiguous()):
+        raise ValueError("probe_rows needs a contiguous uint8 device tensor [S, nrows, L]")
+    S, n, L = stripes.shape
+    _lib.check(_lib.lib().hrs_probe_rows(stripes.data_ptr(), S, n, L, int(nread), int(nwrite), int(blocks_per_cu),
+                                         _stream(stripes)))

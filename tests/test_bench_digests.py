@@ -62,3 +62,11 @@ def test_golden_config2_block0_from_the_oracle():
     _, _, key, par, _ = M.block_job((2, 6, 3, 64 << 10, 0, 256, "parity"))
     with open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")) as f:
         assert json.load(f)["config2"]["parity"][key] == par
+
+
+def test_pattern_fields():
+    import bench
+    probes = {"pattern": {"encode": {"GBps": 5000.0}, "decode": {"error": "not instantiated"}}}
+    assert bench.pattern_fields(probes, "encode", 4500.0) == {"pattern_ceiling": 5000.0, "frac_vs_pattern": 0.9}
+    assert bench.pattern_fields(probes, "decode", 4500.0) == {"pattern_ceiling": None, "frac_vs_pattern": None}
+    assert bench.pattern_fields(probes, "other", 1.0)["frac_vs_pattern"] is None
