@@ -358,7 +358,10 @@ def hbm_probes(dev, stripes=None, patterns=(), nbytes=4 << 30, reps=5):
       pattern : for each (name, nread, nwrite) in `patterns`, the coding
                 kernels' access pattern without the math (hrs_probe_rows) over
                 `stripes` [S, n, L] itself — same buffer, same bytes, same
-                2 KiB-window order. This is the ceiling of the pattern: a 1:1
+                2 KiB-window order — under four load schedules (all loads
+                first; or D rows in flight with VALU filler standing in for
+                the math, which HBM serves better than a burst:
+                tools/pace_probe.hip). This is the ceiling of the pattern: a 1:1
                 copy is not one for the codec's read-heavy mixes, and the mix
                 of the read-only and write-only peaks ((R + W) / (R / read +
                 W / write), mix_ceiling) is optimistic, because HBM pays for
@@ -418,13 +421,15 @@ def hbm_probes(dev, stripes=None, patterns=(), nbytes=4 << 30, reps=5):
         for name, nr, nw in patterns:
             moved = (nr + nw) * L * S
             try:
-                v = {f"{bpc}cu": rate(moved, lambda: device.probe_rows(stripes, nr, nw, bpc)) for bpc in (1, 2, 4)}
+                v = {f"sched{sc}_{bpc}cu": rate(moved, lambda: device.probe_rows(stripes, nr, nw, bpc, sc))
+                     for sc in (0, 1, 2, 3) for bpc in (1, 2)}
             except Exception as e:  # a (nread, nwrite) pair hrs_probe_rows does not instantiate
                 out["pattern"][name] = {"error": str(e)}
                 continue
             out["pattern"][name] = {"GBps": v[best(v)], "best": best(v), "variants": v, "reads": nr, "writes": nw,
                                     "how": f"hrs_probe_rows over the bench's own {S} x {n} x {L} stripes: "
-                                           f"{nr} rows read / {nw} written per 2 KiB window, no math"}
+                                           f"{nr} rows read / {nw} written per 2 KiB window, no GF math; "
+                                           "load schedules 0-3 x 1-2 blocks/CU (include/hrs_probe.h)"}
     return out
 
 

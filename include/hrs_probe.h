@@ -59,12 +59,17 @@ hrs_status hrs_probe_write(void* dst, size_t bytes, int blocks_per_cu, void* str
  * stripes of `nrows` rows of `cell_bytes` each, stripe-major and contiguous
  * from `base` (the layout of encodeBulk's [parity..., data...] rows): per
  * 2 KiB column window, rows [nrows - nread, nrows) are read and rows
- * [0, nwrite) overwritten with their XOR (+ the row index). cell_bytes must be
- * a multiple of 2048 and base of 16 (else HRS_EALIGN); (nread, nwrite) one of
+ * [0, nwrite) overwritten with their XOR (+ the row index). `schedule` sets
+ * how the loads are spaced — D rows in flight per wave and M dependent VALU
+ * steps per loaded dword in place of the GF math, since HBM serves a
+ * spaced-out request stream better than a burst: 0 = all rows' loads first,
+ * no math; 1 = D 3, M 12; 2 = D 5, M 6; 3 = D 1, M 0. cell_bytes must be a
+ * multiple of 2048 and base of 16 (else HRS_EALIGN); (nread, nwrite) one of
  * (10,4) (10,3) (10,2) (10,1) (10,0) (6,3) (12,4) (12,2) (3,2), with
- * nread + nwrite <= nrows (else HRS_EINVAL). Asynchronous on `stream`. */
+ * nread + nwrite <= nrows, schedule in [0, 3] (else HRS_EINVAL). Asynchronous
+ * on `stream`. */
 hrs_status hrs_probe_rows(void* base, size_t nstripes, int nrows, size_t cell_bytes, int nread, int nwrite,
-                          int blocks_per_cu, void* stream);
+                          int schedule, int blocks_per_cu, void* stream);
 
 #ifdef __cplusplus
 }

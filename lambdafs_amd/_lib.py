@@ -112,7 +112,7 @@ def lib():
         "hrs_probe_read": ([P, S, I, P, P], I),
         "hrs_probe_write": ([P, S, I, P], I),
         "hrs_probe_stream": ([I, P, P, S, I, I, I, P], I),
-        "hrs_probe_rows": ([P, S, I, S, I, I, I, P], I),
+        "hrs_probe_rows": ([P, S, I, S, I, I, I, I, P], I),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

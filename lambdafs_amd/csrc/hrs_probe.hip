@@ -8,7 +8,7 @@
 //     (hrs_probe_rows): 2 KiB column windows of `nread` rows of a stripe-major
 //     [S][nrows][L] buffer read, `nwrite` rows written, nontemporal 16-byte
 //     accesses, one wave task per window, as encode_static_kernel and the
-//     pipelined repair kernel walk them.
+//     pipelined repair kernel walk them, under a few load schedules.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -74,10 +74,24 @@ __global__ void __launch_bounds__(256) stream_kernel(const u32x4* __restrict__ s
     if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9E3779B9u && acc[0] == 0x7F4A7C15u) dst[threadIdx.x] = acc;
 }
 
-// The codec's access pattern without the math: task t = (stripe, 2 KiB window);
-// read rows [nrows - R, nrows), write rows [0, W) with the XOR of the reads
-// (+ the row index), every access nontemporal, all R rows' loads issued first.
-template <int R, int W>
+// The codec's access pattern without the GF math: task t = (stripe, 2 KiB
+// window); read rows [nrows - R, nrows), write rows [0, W) with the XOR of the
+// reads (+ the row index), every access nontemporal. D rows' loads in flight
+// (row r + D issued before row r is used; sched_barriers stop the compiler
+// hoisting more) and M dependent VALU steps per loaded dword stand in for the
+// math: HBM serves a spaced-out request stream better than a burst, so the
+// pattern's ceiling is the best of a few schedules, not the all-loads-first
+// one (tools/pace_probe.hip, profiles/r03/ab/NOTES.md).
+template <int M>
+__device__ __forceinline__ u32x4 pace_work(u32x4 x) {
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = __builtin_amdgcn_alignbit(x[q], x[q], 7) ^ (0x9E3779B9u * (m + 1));
+  return x;
+}
+
+template <int R, int W, int D, int M>
 __global__ void __launch_bounds__(256) rows_kernel(uint8_t* __restrict__ base, uint64_t nstripes, int nrows,
                                                     uint64_t L) {
   const int lane = threadIdx.x & 63;
@@ -88,17 +102,21 @@ __global__ void __launch_bounds__(256) rows_kernel(uint8_t* __restrict__ base, u
     const uint64_t s = t / nwin;
     uint8_t* sb = base + s * nrows * L + (t - s * nwin) * 2048u + lane * 16;
     u32x4 v[R][2];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
+    auto ld = [&](int r) {
       const u32x4* p = reinterpret_cast<const u32x4*>(sb + (nrows - R + r) * L);
       v[r][0] = __builtin_nontemporal_load(p);
       v[r][1] = __builtin_nontemporal_load(p + 64);
-    }
-    u32x4 a = v[0][0], b = v[0][1];
+    };
 #pragma unroll
-    for (int r = 1; r < R; ++r) {
-      a ^= v[r][0];
-      b ^= v[r][1];
+    for (int r = 0; r < D && r < R; ++r) ld(r);
+    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r + D < R) ld(r + D);
+      __builtin_amdgcn_sched_barrier(0);
+      a ^= pace_work<M>(v[r][0]);
+      b ^= pace_work<M>(v[r][1]);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int o = 0; o < W; ++o) {
@@ -132,13 +150,26 @@ hrs_status launch_stream(const void* src, void* dst, size_t bytes, int chunk_kib
   }
 }
 
-template <int R, int W>
-hrs_status launch_rows_rw(void* base, size_t nstripes, int nrows, size_t L, unsigned grid, hipStream_t st) {
-  note_kernel_t("probe_rows_kernel", R, W);
-  auto k = rows_kernel<R, W>;
+// Schedules (rows in flight D, VALU steps per dword M): 0 = (R, 0) all loads
+// first, no math; 1 = (3, 12); 2 = (5, 6); 3 = (1, 0).
+template <int R, int W, int D, int M>
+hrs_status launch_rows_dm(void* base, size_t nstripes, int nrows, size_t L, unsigned grid, hipStream_t st) {
+  note_kernel_t("probe_rows_kernel", R, W, D, M);
+  auto k = rows_kernel<R, W, D, M>;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<uint8_t*>(base), static_cast<uint64_t>(nstripes),
                      nrows, static_cast<uint64_t>(L));
   return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
+}
+
+template <int R, int W>
+hrs_status launch_rows_rw(void* base, size_t nstripes, int nrows, size_t L, int schedule, unsigned grid,
+                          hipStream_t st) {
+  switch (schedule) {
+    case 0: return launch_rows_dm<R, W, R, 0>(base, nstripes, nrows, L, grid, st);
+    case 1: return launch_rows_dm<R, W, 3, 12>(base, nstripes, nrows, L, grid, st);
+    case 2: return launch_rows_dm<R, W, 5, 6>(base, nstripes, nrows, L, grid, st);
+    default: return launch_rows_dm<R, W, 1, 0>(base, nstripes, nrows, L, grid, st);
+  }
 }
 
 bool stream_args_ok(int chunk_kib, int bpc) {
@@ -176,8 +207,9 @@ extern "C" hrs_status hrs_probe_write(void* dst, size_t bytes, int blocks_per_cu
 }
 
 extern "C" hrs_status hrs_probe_rows(void* base, size_t nstripes, int nrows, size_t cell_bytes, int nread,
-                                     int nwrite, int blocks_per_cu, void* stream) {
-  if (blocks_per_cu < 1 || blocks_per_cu > 32 || nrows < 1 || nread < 1 || nwrite < 0 || nread + nwrite > nrows)
+                                     int nwrite, int schedule, int blocks_per_cu, void* stream) {
+  if (blocks_per_cu < 1 || blocks_per_cu > 32 || nrows < 1 || nread < 1 || nwrite < 0 || nread + nwrite > nrows ||
+      schedule < 0 || schedule > 3)
     return HRS_EINVAL;
   if (nstripes && !base) return HRS_EINVAL;
   if ((reinterpret_cast<uintptr_t>(base) & 15u) || (cell_bytes % 2048u)) return HRS_EALIGN;
@@ -187,15 +219,15 @@ extern "C" hrs_status hrs_probe_rows(void* base, size_t nstripes, int nrows, siz
   // The read / write counts of the shapes bench.py and the tests quote:
   // RS(10,4) encode and 1..4-erasure repairs, RS(6,3), RS(12,4), RS(3,2).
   switch (nread * 100 + nwrite) {
-    case 1004: return hrs::launch_rows_rw<10, 4>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 1003: return hrs::launch_rows_rw<10, 3>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 1002: return hrs::launch_rows_rw<10, 2>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 1001: return hrs::launch_rows_rw<10, 1>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 1000: return hrs::launch_rows_rw<10, 0>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 603: return hrs::launch_rows_rw<6, 3>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 1204: return hrs::launch_rows_rw<12, 4>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 1202: return hrs::launch_rows_rw<12, 2>(base, nstripes, nrows, cell_bytes, grid, st);
-    case 302: return hrs::launch_rows_rw<3, 2>(base, nstripes, nrows, cell_bytes, grid, st);
+    case 1004: return hrs::launch_rows_rw<10, 4>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 1003: return hrs::launch_rows_rw<10, 3>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 1002: return hrs::launch_rows_rw<10, 2>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 1001: return hrs::launch_rows_rw<10, 1>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 1000: return hrs::launch_rows_rw<10, 0>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 603: return hrs::launch_rows_rw<6, 3>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 1204: return hrs::launch_rows_rw<12, 4>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 1202: return hrs::launch_rows_rw<12, 2>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
+    case 302: return hrs::launch_rows_rw<3, 2>(base, nstripes, nrows, cell_bytes, schedule, grid, st);
     default: return HRS_EINVAL;
   }
 }

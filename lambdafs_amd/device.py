@@ -233,14 +233,15 @@ def probe_write(dst, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
                                            int(bool(nontemporal)), int(blocks_per_cu), _stream(dst)))
 
 
-def probe_rows(stripes, nread, nwrite, blocks_per_cu=2):
+def probe_rows(stripes, nread, nwrite, blocks_per_cu=2, schedule=0):
     """The coding kernels' access pattern without the math (hrs_probe_rows):
     `stripes` is a contiguous uint8 device tensor [S, nrows, L]; per 2 KiB
     column window rows [nrows - nread, nrows) are read and rows [0, nwrite)
-    overwritten with their XOR (+ the row index)."""
+    overwritten with their XOR (+ the row index); `schedule` 0-3 spaces the
+    loads (include/hrs_probe.h)."""
     if (not stripes.is_cuda or stripes.dtype != _lib.torch.uint8 or stripes.dim() != 3
             or not stripes.is_contiguous()):
         raise ValueError("probe_rows needs a contiguous uint8 device tensor [S, nrows, L]")
     S, n, L = stripes.shape
-    _lib.check(_lib.lib().hrs_probe_rows(stripes.data_ptr(), S, n, L, int(nread), int(nwrite), int(blocks_per_cu),
-                                         _stream(stripes)))
+    _lib.check(_lib.lib().hrs_probe_rows(stripes.data_ptr(), S, n, L, int(nread), int(nwrite), int(schedule),
+                                         int(blocks_per_cu), _stream(stripes)))

@@ -31,15 +31,17 @@ def test_rows_argument_checks():
     L = _lib.lib()
     buf = ctypes.create_string_buffer(4096)
     p16 = (ctypes.addressof(buf) + 15) & ~15
-    einval = L.hrs_probe_rows(p16, 1, 14, 2048, 11, 4, 2, None)  # 11 + 4 > 14
+    einval = L.hrs_probe_rows(p16, 1, 14, 2048, 11, 4, 0, 2, None)  # 11 + 4 > 14
     assert einval != 0
-    assert L.hrs_probe_rows(p16, 1, 14, 2048, 10, 4, 0, None) == einval  # blocks per CU
-    assert L.hrs_probe_rows(p16, 1, 14, 2048, 0, 1, 2, None) == einval
-    assert L.hrs_probe_rows(p16, 1, 20, 2048, 9, 4, 2, None) == einval  # pair not instantiated
-    ealign = L.hrs_probe_rows(p16, 1, 14, 1000, 10, 4, 2, None)
+    assert L.hrs_probe_rows(p16, 1, 14, 2048, 10, 4, 0, 0, None) == einval  # blocks per CU
+    assert L.hrs_probe_rows(p16, 1, 14, 2048, 0, 1, 0, 2, None) == einval
+    assert L.hrs_probe_rows(p16, 1, 20, 2048, 9, 4, 0, 2, None) == einval  # pair not instantiated
+    ealign = L.hrs_probe_rows(p16, 1, 14, 1000, 10, 4, 0, 2, None)
     assert ealign not in (0, einval)
-    assert L.hrs_probe_rows(p16 + 1, 1, 14, 2048, 10, 4, 2, None) == ealign
-    assert L.hrs_probe_rows(p16, 0, 14, 2048, 10, 4, 2, None) == 0
+    assert L.hrs_probe_rows(p16 + 1, 1, 14, 2048, 10, 4, 0, 2, None) == ealign
+    assert L.hrs_probe_rows(p16, 1, 14, 2048, 10, 4, 4, 2, None) == einval  # schedule
+    assert L.hrs_probe_rows(p16, 1, 14, 2048, 10, 4, -1, 2, None) == einval
+    assert L.hrs_probe_rows(p16, 0, 14, 2048, 10, 4, 0, 2, None) == 0
 
 
 @pytest.mark.gpu
@@ -63,17 +65,22 @@ def test_stream_shapes_move_every_byte(cuda, chunk, nt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("schedule", [0, 1, 2, 3])
 @pytest.mark.parametrize("nr,nw,n", [(10, 4, 14), (10, 1, 14), (6, 3, 9), (12, 2, 16), (3, 2, 5)])
-def test_rows_pattern_reads_and_writes_the_claimed_rows(cuda, nr, nw, n):
+def test_rows_pattern_reads_and_writes_the_claimed_rows(cuda, nr, nw, n, schedule):
+    """Schedules 0 and 3 write the plain XOR of the read rows (+ o); 1 and 2
+    pass each loaded word through their VALU filler first, so there only the
+    rows touched and the + o between written rows are checked."""
     torch = cuda
     S, L = 5, 3 * 2048
     st = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device="cuda")
     before = st.cpu().numpy()
-    device.probe_rows(st, nr, nw, 2)
+    device.probe_rows(st, nr, nw, 2, schedule)
     after = st.cpu().numpy()
     x = np.bitwise_xor.reduce(before[:, n - nr:, :], axis=1).view(np.uint32)  # [S, L/4]
+    w0 = after[:, 0, :].view(np.uint32) if nw else None
     for o in range(nw):
-        # each 16-byte element = XOR of the read rows' elements + o, per 32-bit word
-        want = (x.astype(np.uint64) + o).astype(np.uint32).view(np.uint8)
-        assert np.array_equal(after[:, o, :], want), o
+        got = after[:, o, :].view(np.uint32)
+        base = x if schedule in (0, 3) else w0
+        assert np.array_equal(got, (base.astype(np.uint64) + o).astype(np.uint32)), o
     assert np.array_equal(after[:, nw:, :], before[:, nw:, :])  # nothing else touched
