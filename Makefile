@@ -49,11 +49,16 @@ build/hrs_fused.o: lambdafs_amd/csrc/hrs_fused.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -mllvm -pragma-unroll-threshold=1000000 -c $< -o $@
 
+build/hrs_decode_crc.o: lambdafs_amd/csrc/hrs_decode_crc.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 build/hrs_probe.o: lambdafs_amd/csrc/hrs_probe.hip include/hrs_probe.h $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_probe.o
+KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_decode_crc.o \
+            build/hrs_probe.o
 
 $(LIB): $(API_OBJ) $(KOBJ) lambdafs_amd/csrc/libhrs.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs.map -o $@ $(API_OBJ) $(KOBJ)

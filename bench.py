@@ -623,6 +623,20 @@ def run(args):
     fused_ms = med_ms(lambda: device.encode_stripes_crc(code, stripes), reps)
     two_ms = med_ms(lambda: (device.encode_stripes(code, stripes), device.crc32_rows(code, cells)), reps)
 
+    # ... and the Decoder's check of a repaired block (Decoder.java:222-229,
+    # :645-655): repair + CRC-32 of the repaired cells fused
+    # (hrs_decode_crc_dev) vs the repair then hrs_crc32_dev over its outputs
+    out_crc = torch.empty_like(out)
+    dcrc_fused = device.decode_stripes_crc(code, stripes, erased, ntr, out_crc)
+    dfused_kernel = code.lastKernel()
+    dcrc_two = device.crc32_rows(code, [out[:, 0, :]])
+    if not parallel.all_ok(bool(torch.equal(out_crc, out)) and bool(torch.equal(dcrc_fused, dcrc_two)), dev):
+        raise RuntimeError("fused decode+CRC differs from decode then CRC")
+    dfused_ms = med_ms(lambda: device.decode_stripes_crc(code, stripes, erased, ntr, out_crc), reps)
+    dtwo_ms = med_ms(lambda: (device.apply_rows(code, D_live, in_rows, out_rows),
+                              device.crc32_rows(code, [out[:, 0, :]])), reps)
+    del out_crc
+
     # the timed outputs against the oracle: parity and decoded rows per block
     # of 256 global stripes vs tests/golden/bench_digests.json
     sha = None
@@ -724,6 +738,15 @@ def run(args):
                 "fused_GBps_algorithmic": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9, 1),
                 "fused_frac": round(enc_bytes / (float(np.median(fused_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "speedup_vs_two_pass": round(float(np.median(two_ms)) / float(np.median(fused_ms)), 3),
+            },
+            "decode_crc": {
+                "what": "repair of data shard 0 + java.util.zip.CRC32 of the repaired cell (Decoder's block check)",
+                "kernel": traffic_key(dfused_kernel) + " + crc_fold_kernel",
+                "fused_ms": stats(dfused_ms),
+                "two_pass_ms": stats(dtwo_ms),
+                "fused_GBps_algorithmic": round(dec_bytes / (float(np.median(dfused_ms)) * 1e-3) / 1e9, 1),
+                "fused_frac": round(dec_bytes / (float(np.median(dfused_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "speedup_vs_two_pass": round(float(np.median(dtwo_ms)) / float(np.median(dfused_ms)), 3),
             },
             "hbm_probes": probes,
             "parity_sha256": sha,

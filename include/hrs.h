@@ -323,6 +323,21 @@ hrs_status hrs_encode_crc_dev(hrs_codec* codec, const uint8_t* const* in_rows, s
                               uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
                               const uint32_t* crc_in, uint32_t* crc_out, void* stream);
 
+/* Repair + CRC-32 of the repaired cells in one pass (Decoder: decodeBulk, then
+ * the repaired block's CRC32 compared with the NameNode's checksum;
+ * Decoder.java:222-229, :352-353, :645-655). Same rows and semantics as
+ * hrs_decode_dev; crc_out[s * num_erased + t] = CRC32 of output t of stripe
+ * s, continuing from crc_in (same layout; NULL = fresh). DEVICE crc arrays.
+ * Repairs of <= 4 locations from <= 12 live survivors (<= 8 at 4 outputs),
+ * len a multiple of 2 KiB and 16-byte-aligned rows take one fused kernel
+ * (each repaired cell written once, never read back); anything else runs
+ * hrs_decode_dev then the CRC pass, with identical results. Asynchronous on
+ * `stream`. */
+hrs_status hrs_decode_crc_dev(hrs_codec* codec, const uint8_t* const* rows, size_t in_stride,
+                              uint8_t* const* out_rows, size_t out_stride, const int* erased, int num_erased,
+                              const int* not_to_read, int num_not_to_read, size_t len, size_t nstripes,
+                              const uint32_t* crc_in, uint32_t* crc_out, void* stream);
+
 /* Kernel selection for tests and benchmarks: 0 = auto (default), 1 = force
  * the runtime-matrix bit-sliced kernel, 2 = force the byte-granular kernel,
  * 3 = auto, except that hrs_encode_crc_dev takes the fused kernel whenever the

@@ -36,7 +36,7 @@ EXPORTS = (
     "hrs_locations_to_read", "hrs_encode_matrix", "hrs_decode_matrix",
     "hrs_encode", "hrs_decode", "hrs_decode3", "hrs_encode_crc", "hrs_decode_crc",
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
-    "hrs_encode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
+    "hrs_encode_crc_dev", "hrs_decode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
     "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_probe_copy", "hrs_probe_read", "hrs_probe_write", "hrs_wait",
     "hrs_probe_stream", "hrs_probe_rows",
@@ -98,6 +98,7 @@ def lib():
         "hrs_apply_dev": ([P, U8P, I, I, PP, S, PP, S, S, S, P], I),
         "hrs_crc32_dev": ([P, PP, I, S, S, S, P, P, P], I),
         "hrs_encode_crc_dev": ([P, PP, S, PP, S, S, S, P, P, P], I),
+        "hrs_decode_crc_dev": ([P, PP, S, PP, S, IP, I, IP, I, S, S, P, P, P], I),
         "hrs_decode_batch_host": ([P, P, S, S, P, I, P, S, S, S, S], I),
         "hrs_encode_batch_host": ([P, P, S, S, S, S], I),
         "hrs_encode_submit": ([P, PP, S, I, ctypes.POINTER(ctypes.c_uint64)], I),

@@ -161,6 +161,9 @@ hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strid
 hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
                            size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
                            hipStream_t s, uint32_t* raw);
+hrs_status apply_crc_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                          size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
+                          const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw);
 
 }  // namespace hrs::api
 #pragma GCC visibility pop

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "crc32.hpp"
+#include "hrs_internal.hpp"
 
 namespace hrs {
 
@@ -95,5 +96,17 @@ struct EncodeCrcArgs {
 // (family, k, p) has no fused kernel (the caller runs encode, then CRC).
 hipError_t launch_encode_crc(int family, int k, int p, const EncodeCrcArgs& a, int cus, hipStream_t s,
                              bool* handled);
+
+// Fused repair + CRC-32 (hrs_decode_crc.hip): the runtime-matrix apply of
+// `r` (whole 2 KiB windows: r.nwin = len / 2 KiB, no accumulate) with the raw
+// CRC of every output's window in raw[stripe][output][window]
+// (crc_fold_kernel finishes them with 2 KiB windows). *handled = false for
+// shapes without a fused kernel (> 4 outputs, > 12 inputs, > 8 at 4 outputs).
+struct DecodeCrcArgs {
+  RowArgs r;
+  uint32_t* raw;
+  const uint32_t* tables;  // kCrcLdsWordsA words (device)
+};
+hipError_t launch_decode_crc(const DecodeCrcArgs& d, int cus, hipStream_t s, bool* handled);
 
 }  // namespace hrs

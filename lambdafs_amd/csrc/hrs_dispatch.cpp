@@ -442,6 +442,63 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
   return run_crc(c, rows.data(), strides.data(), n, len, nstripes, crc_in, crc_out, s, raw);
 }
 
+// out_o = XOR_i m[o][i] * in_i for every stripe, plus the CRC-32 of every
+// output row (crc_out[s * nout + o], continuing crc_in): the Decoder's repair
+// and the checksum of the repaired cells, with raw window CRCs in `raw`
+// (crc_raw_bytes_for(len, nstripes, nout)). Fused (hrs_decode_crc.hip) for
+// the pipelined repair shapes on whole 2 KiB windows and aligned rows; else
+// the apply, then the CRC pass over its outputs.
+hrs_status apply_crc_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                          size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
+                          const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw) {
+  if (nout < 0 || nin < 0 || nout > 255 || nin > 255) return fail(c, HRS_EINVAL, "bad matrix shape %dx%d", nout, nin);
+  if (nout == 0 || nstripes == 0) return HRS_OK;
+  for (int o = 0; o < nout; ++o)
+    if (!out_rows[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  std::vector<int> live;
+  for (int i = 0; i < nin; ++i) {
+    bool any = false;
+    for (int o = 0; o < nout; ++o) any |= m[o * nin + i] != 0;
+    if (any) live.push_back(i);
+  }
+  const int nlive = static_cast<int>(live.size());
+  bool fused = (c->kernel_mode == 0 || c->kernel_mode == 3) && len > 0 && len % hrs::kWindowBytes == 0 &&
+               nlive >= 1 && nout <= 4 && nlive <= (nout == 4 ? 8 : 12) && in_stride % 16 == 0 &&
+               out_stride % 16 == 0;
+  for (int i : live) fused &= in_rows[i] != nullptr && aligned16(in_rows[i]);
+  for (int o = 0; o < nout && fused; ++o) fused &= aligned16(out_rows[o]);
+  if (fused) {
+    hrs_status st = crc_window_tables(c);
+    if (st != HRS_OK) return st;
+    hrs::DecodeCrcArgs d{};
+    for (int j = 0; j < nlive; ++j) d.r.in[j] = in_rows[live[j]];
+    for (int o = 0; o < nout; ++o) {
+      d.r.out[o] = out_rows[o];
+      for (int j = 0; j < nlive; ++j) hrs::set_coef(d.r, o, j, m[o * nin + live[j]]);
+    }
+    d.r.in_stride = in_stride;
+    d.r.out_stride = out_stride;
+    d.r.len = len;
+    d.r.nwin = len / hrs::kWindowBytes;
+    d.r.ntasks = d.r.nwin * nstripes;
+    d.r.nin = nlive;
+    d.r.nout = nout;
+    d.raw = raw;
+    d.tables = c->crc_tables_a;
+    bool handled = false;
+    hipError_t e = hrs::launch_decode_crc(d, hrs::device_cu_count(), s, &handled);
+    if (e != hipSuccess) return hip_fail(c, e, "fused decode+crc launch");
+    if (handled) {
+      c->last_kernel = hrs::last_kernel();
+      return crc_fold(c, len, nstripes * nout, crc_in, crc_out, s, raw, hrs::kWindowBytes);
+    }
+  }
+  hrs_status st = run_apply(c, m, nout, nin, in_rows, in_stride, out_rows, out_stride, len, nstripes, s, false);
+  if (st != HRS_OK) return st;
+  std::vector<size_t> strides(nout, out_stride);
+  return run_crc(c, out_rows, strides.data(), nout, len, nstripes, crc_in, crc_out, s, raw);
+}
+
 }  // namespace hrs::api
 
 using namespace hrs::api;
@@ -509,6 +566,26 @@ hrs_status hrs_decode_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_st
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   return run_apply(c, d, ne, c->n, rows, in_stride, out_rows, out_stride, len, nstripes,
                    static_cast<hipStream_t>(stream), false);
+}
+
+hrs_status hrs_decode_crc_dev(hrs_codec* c, const uint8_t* const* rows, size_t in_stride, uint8_t* const* out_rows,
+                              size_t out_stride, const int* erased, int ne, const int* ntr, int nn, size_t len,
+                              size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, void* stream) {
+  if (!c) return HRS_EINVAL;
+  if (!rows || ne < 0 || nn < 0 || (ne > 0 && (!out_rows || !erased || !crc_out)) || (nn > 0 && !ntr))
+    return fail(c, HRS_EINVAL, "bad decode arguments");
+  if (ne == 0 || nstripes == 0) return HRS_OK;
+  std::vector<uint8_t> tmp;
+  const uint8_t* d = nullptr;
+  hrs_status st = decode5_matrix(c, erased, ne, ntr, nn, rows, tmp, &d);
+  if (st != HRS_OK) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  st = crc_scratch(c, crc_raw_bytes_for(len, nstripes, ne), s);
+  if (st != HRS_OK) return st;
+  return crc_scratch_release(c, s, apply_crc_impl(c, d, ne, c->n, rows, in_stride, out_rows, out_stride, len, nstripes,
+                                                  crc_in, crc_out, s, c->crc_raw));
 }
 
 hrs_status hrs_apply_dev(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,

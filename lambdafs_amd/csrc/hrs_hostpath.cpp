@@ -154,14 +154,11 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
     if (crc.mode == kCrcEncode)
       st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+    else if (crc.mode == kCrcOutputs)  // repair + CRC of the repaired cells (fused where the shape allows)
+      st = apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
     else
       st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
     if (st != HRS_OK) return st;
-    if (crc.mode == kCrcOutputs) {
-      std::vector<size_t> strides(nout, 0);
-      st = run_crc(c, dout.data(), strides.data(), nout, lj, 1, nullptr, dcrc, h.stream, draw);
-      if (st != HRS_OK) return st;
-    }
     // outputs (and the chunk CRCs right behind them) back to the staging
     const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + lj;
     hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost, h.stream);
@@ -257,14 +254,11 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
   uint32_t* draw = reinterpret_cast<uint32_t*>(a.dev + raw_off);
   if (crc_mode == kCrcEncode)
     st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, a.stream, draw);
+  else if (crc_mode == kCrcOutputs)
+    st = apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, a.stream, draw);
   else
     st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, a.stream, static_kp);
   if (st != HRS_OK) return st;
-  if (crc_mode == kCrcOutputs) {
-    std::vector<size_t> strides(nout, 0);
-    st = run_crc(c, dout.data(), strides.data(), nout, len, 1, nullptr, dcrc, a.stream, draw);
-    if (st != HRS_OK) return st;
-  }
   const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + len;
   hipError_t e = hipMemcpyAsync(a.pin + pitch * nlive, a.dev + pitch * nlive, back, hipMemcpyDeviceToHost, a.stream);
   if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");

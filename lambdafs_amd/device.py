@@ -101,6 +101,33 @@ def decode_stripes(code, stripes, erased, not_to_read, out):
         int_array(not_to_read), len(not_to_read), L, S, _stream(stripes)))
 
 
+def decode_stripes_crc(code, stripes, erased, not_to_read, out, crc_in=None):
+    """decode_stripes plus the CRC-32 (java.util.zip.CRC32) of every repaired
+    cell in one pass, as the Decoder checks a repaired block against the
+    NameNode's checksum (Decoder.java:222-229, :645-655): returns an int32
+    tensor [S, e] of the uint32 CRC bits; crc_in (same layout) continues
+    running CRCs across successive cells."""
+    torch = _lib.torch
+    n = code.stripeSize() + code.paritySize()
+    if stripes.dim() != 3 or stripes.shape[1] != n:
+        raise ValueError(f"stripes must be [S, {n}, L]")
+    ntr = set(not_to_read)
+    rows, s_in, L, S = _rows([None if loc in ntr else stripes[:, loc, :] for loc in range(n)])
+    outs, s_out, L2, S2 = _rows([out[:, i, :] for i in range(len(erased))])
+    if (L, S) != (L2, S2):
+        raise ValueError("out must be [S, e, L]")
+    crc = torch.empty((S, len(erased)), dtype=torch.int32, device=stripes.device)
+    cin = None
+    if crc_in is not None:
+        if crc_in.shape != crc.shape or crc_in.dtype != torch.int32 or not crc_in.is_contiguous():
+            raise ValueError(f"crc_in must be a contiguous int32 tensor [S, {len(erased)}]")
+        cin = crc_in.data_ptr()
+    code._check(_lib.lib().hrs_decode_crc_dev(
+        code._handle(), rows, s_in, outs, s_out, int_array(erased), len(erased),
+        int_array(not_to_read), len(not_to_read), L, S, cin, crc.data_ptr(), _stream(stripes)))
+    return crc
+
+
 def decode_batch(code, stripes, erased, out):
     """Repair every stripe of stripes[S, n, L] from its own erasure list, in one
     launch (hrs_decode_batch_dev): erased is an int array [S, E] of hops
