@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "hrs_device.hpp"
 #include "hrs_launch.hpp"
@@ -43,15 +44,13 @@ __device__ __forceinline__ void dc_load_task(const RowArgs& a, uint64_t t, int n
     if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
 }
 
+// The repair of task t: slice, multiply, un-slice and store its outputs;
+// acc keeps the stored words for dc_crc_task.
 template <int NOUT, int NINB>
-__device__ __forceinline__ void dc_apply_task(const DecodeCrcArgs& d, uint64_t t, int nin, int lane,
-                                              const SliceTab& slices, const uint32_t* zchunk, const uint32_t* tree,
-                                              uint32_t (&rows)[NINB][8]) {
-  const RowArgs& a = d.r;
+__device__ __forceinline__ void dc_apply_task(const RowArgs& a, uint64_t t, int nin, int lane,
+                                              uint32_t (&rows)[NINB][8], uint32_t (&acc)[NOUT][8]) {
   const uint64_t stripe = t / a.nwin;
-  const uint64_t w = t - stripe * a.nwin;
-  const uint64_t off = w * kWindowBytes;
-  uint32_t acc[NOUT][8];
+  const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
 #pragma unroll
   for (int o = 0; o < NOUT; ++o)
 #pragma unroll
@@ -65,16 +64,30 @@ __device__ __forceinline__ void dc_apply_task(const DecodeCrcArgs& d, uint64_t t
     bitslice(acc[o]);
     store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
   }
+}
+
+// The raw CRC of task t's output windows: the lane's two pieces (slicing-by-4
+// chains), joined with Z_1024, then the 6-level lane tree; lane 0 writes it.
+// A chain of dependent LDS lookups and cross-lane shuffles (~1,500 cycles),
+// so the kernel issues the NEXT task's loads before it (they would otherwise
+// wait behind it and the wave would keep one window in flight instead of two).
+template <int NOUT, bool DPP>
+__device__ __forceinline__ void dc_crc_task(const DecodeCrcArgs& d, uint64_t t, int lane, const SliceTab& slices,
+                                            const uint32_t* zchunk, const uint32_t* tree,
+                                            const uint32_t (&acc)[NOUT][8]) {
+  const uint64_t stripe = t / d.r.nwin;
+  const uint64_t w = t - stripe * d.r.nwin;
   uint32_t c0[NOUT], c1[NOUT];
   rows_piece_crcs<NOUT>(slices, acc, c0, c1);
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-    const uint32_t c = lane_tree(tree, zmul_xor(zchunk, c0[o], c1[o]));
-    if (lane == 0) d.raw[(stripe * NOUT + o) * a.nwin + w] = c;
+    const uint32_t x = zmul_xor(zchunk, c0[o], c1[o]);
+    const uint32_t c = DPP ? lane_tree_dpp(tree, x) : lane_tree(tree, x);
+    if (lane == 0) d.raw[(stripe * NOUT + o) * d.r.nwin + w] = c;
   }
 }
 
-template <int NOUT, int NINB>
+template <int NOUT, int NINB, bool DPP>
 __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const DecodeCrcArgs d) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   for (int i = threadIdx.x; i < kCrcLdsWordsA; i += kDecCrcThreads) lds[i] = d.tables[i];
@@ -90,34 +103,123 @@ __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const D
   uint64_t t = wave_id_in_grid();
   if (t >= a.ntasks) return;
   uint32_t ra[NINB][8], rb[NINB][8];
+  uint32_t acc[NOUT][8];
   dc_load_task<NOUT, NINB>(a, t, nin, lane, ra);
-  for (;;) {  // every wave leaves once its next task index passes ntasks
-    const uint64_t t1 = t + nwaves;
-    if (t1 < a.ntasks) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
-    dc_apply_task<NOUT, NINB>(d, t, nin, lane, slices, zchunk, tree, ra);
-    if (t1 >= a.ntasks) break;
+  uint64_t t1 = t + nwaves;
+  if (t1 < a.ntasks) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
+  for (;;) {  // ra: task t, rb: task t1 in flight; every wave leaves once a task index passes ntasks
+    dc_apply_task<NOUT, NINB>(a, t, nin, lane, ra, acc);
     const uint64_t t2 = t1 + nwaves;
     if (t2 < a.ntasks) dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
-    dc_apply_task<NOUT, NINB>(d, t1, nin, lane, slices, zchunk, tree, rb);
+    dc_crc_task<NOUT, DPP>(d, t, lane, slices, zchunk, tree, acc);
+    if (t1 >= a.ntasks) break;
+    dc_apply_task<NOUT, NINB>(a, t1, nin, lane, rb, acc);
+    const uint64_t t3 = t2 + nwaves;
+    if (t3 < a.ntasks) dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
+    dc_crc_task<NOUT, DPP>(d, t1, lane, slices, zchunk, tree, acc);
     if (t2 >= a.ntasks) break;
     t = t2;
+    t1 = t3;
   }
+}
+
+// HRS_DCRC_TREE=0 (A/B runs): the lane tree's in-row levels by ds_bpermute
+// (lane_tree) instead of DPP moves (lane_tree_dpp).
+bool dcrc_dpp() {
+  static const bool v = [] {
+    const char* e = getenv("HRS_DCRC_TREE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// Plain (not pipelined) form for 2-4 outputs: the pipelined kernel's two row
+// sets + outputs + CRC state exceed the register file there (<2,12>: 253
+// VGPRs and 51 SGPRs spilled, 1.6x the plain repair; profiles/r03/ab/NOTES.md, decode_crc/).
+// One row set; the other waves of the SIMD cover the CRC tail. THREADS = 768
+// (3 waves/SIMD, <= 153 VGPRs) or 512 (2).
+template <int NOUT, int NINB, int THREADS>
+__global__ void __launch_bounds__(THREADS) decode_crc_kernel(const DecodeCrcArgs d) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  for (int i = threadIdx.x; i < kCrcLdsWordsA; i += THREADS) lds[i] = d.tables[i];
+  __syncthreads();
+  const RowArgs& a = d.r;
+  const int lane = threadIdx.x & 63;
+  const SliceTab slices = slice_tab(lane);
+  const uint32_t* zchunk = lds + kCrcSliceWords;
+  const uint32_t* tree = zchunk + 1024;
+  const uint32_t nwaves = gridDim.x * (THREADS / 64);
+  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+    int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
+    asm volatile("" : "+s"(nin));
+    // written out, not through dc_load_task / dc_apply_task: with the helpers
+    // the 2- and 4-output forms compile to thousands of v_mov_b64 shuffling the
+    // accumulators between registers at every coefficient branch
+    const uint64_t stripe = t / a.nwin;
+    const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+    const uint64_t in_base = stripe * a.in_stride + off;
+    uint32_t rows[NINB][8];
+#pragma unroll
+    for (int r = 0; r < NINB; ++r)
+      if (r < nin) load_row(a.in[r] + in_base, lane, rows[r]);
+    uint32_t acc[NOUT][8];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[o][q] = 0u;
+#pragma unroll
+    for (int r = 0; r < NINB; ++r)
+      if (r < nin) accumulate_row<NOUT, NINB>(acc, rows[r], a.cw[r]);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      bitslice(acc[o]);
+      store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+    }
+    dc_crc_task<NOUT, true>(d, t, lane, slices, zchunk, tree, acc);
+  }
+}
+
+// 768 threads (3 waves/SIMD) measured 3-10% faster than 512 for the 2- and
+// 3-output repairs (profiles/r03/ab/decode_crc/v7_plain_inline_512_vs_768.jsonl); HRS_DCRC_THREADS=512
+// for A/B runs.
+int dcrc_threads() {
+  static const int v = [] {
+    const char* e = getenv("HRS_DCRC_THREADS");
+    return (e && atoi(e) == 512) ? 512 : 768;
+  }();
+  return v;
 }
 
 template <int NOUT, int NINB>
 hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
-  auto kern = decode_crc_pipe_kernel<NOUT, NINB>;
-  const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     static_cast<int>(shm));
-  if (e != hipSuccess) return e;
-  note_kernel_t("decode_crc_pipe_kernel", NOUT, NINB);
-  constexpr uint64_t per_block = kDecCrcThreads / 64;
-  uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
-  if (g > static_cast<uint64_t>(cus)) g = cus;
-  if (g == 0) g = 1;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(kDecCrcThreads), shm, s, d);
-  return hipGetLastError();
+  if constexpr (NOUT >= 2) {
+    const int threads = dcrc_threads();
+    auto kern = threads == 768 ? decode_crc_kernel<NOUT, NINB, 768> : decode_crc_kernel<NOUT, NINB, 512>;
+    const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm));
+    if (e != hipSuccess) return e;
+    note_kernel_t("decode_crc_kernel", NOUT, NINB, threads);
+    const uint64_t per_block = threads / 64;
+    uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
+    if (g > static_cast<uint64_t>(cus)) g = cus;
+    if (g == 0) g = 1;
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, d);
+    return hipGetLastError();
+  } else {
+    auto kern = dcrc_dpp() ? decode_crc_pipe_kernel<NOUT, NINB, true> : decode_crc_pipe_kernel<NOUT, NINB, false>;
+    const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(shm));
+    if (e != hipSuccess) return e;
+    note_kernel_t("decode_crc_pipe_kernel", NOUT, NINB);
+    constexpr uint64_t per_block = kDecCrcThreads / 64;
+    uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
+    if (g > static_cast<uint64_t>(cus)) g = cus;
+    if (g == 0) g = 1;
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(kDecCrcThreads), shm, s, d);
+    return hipGetLastError();
+  }
 }
 
 template <int NOUT>

@@ -329,6 +329,29 @@ __device__ __forceinline__ uint32_t lane_tree(const uint32_t* tree, uint32_t c) 
   return c;
 }
 
+// Lane l receives v of lane l + N within its row of 16 lanes (0 past the
+// row's end): one DPP row_shl move on the VALU instead of a ds_bpermute
+// through the LDS unit.
+template <int N>
+__device__ __forceinline__ uint32_t dpp_down(uint32_t v) {
+  static_assert(N >= 1 && N <= 15, "row_shl reaches within a row of 16 lanes");
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x100 + N, 0xF, 0xF, true));
+}
+
+// lane_tree with the levels inside a 16-lane row (2^t = 1, 2, 4, 8) moved by
+// DPP: lane 0's chain only ever reads lanes of its own row at those levels
+// (lanes whose partner lies past their row end compute values no later level
+// reads). Same result as lane_tree in lane 0.
+__device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* tree, uint32_t c) {
+  c = zmul(tree + 0 * 1024, c) ^ dpp_down<1>(c);
+  c = zmul(tree + 1 * 1024, c) ^ dpp_down<2>(c);
+  c = zmul(tree + 2 * 1024, c) ^ dpp_down<4>(c);
+  c = zmul(tree + 3 * 1024, c) ^ dpp_down<8>(c);
+  c = zmul(tree + 4 * 1024, c) ^ __shfl_down(c, 16, 64);
+  c = zmul(tree + 5 * 1024, c) ^ __shfl_down(c, 32, 64);
+  return c;
+}
+
 // ---------------------------------------- runtime-matrix kernel helpers
 
 // NINB >= nin rows of the window are all loaded before any math (one

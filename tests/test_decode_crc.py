@@ -97,7 +97,7 @@ def test_fused_repairs_vs_oracle(cuda, k, p):
         _check_vs_oracle(k, p, host, got, erased, to_read, ntr, range(S))
         live = int((code.decodeMatrix(erased, ntr) != 0).any(axis=0).sum())  # columns the kernel reads
         fused = live <= (8 if len(erased) == 4 else 12)
-        assert _run.kernel.startswith("decode_crc_pipe_kernel") == fused, (erased, _run.kernel)
+        assert _run.kernel.startswith("decode_crc") == fused, (erased, _run.kernel)
 
 
 @pytest.mark.gpu
@@ -171,7 +171,7 @@ def test_fallback_and_edges(cuda, case):
     to_read, ntr = _pattern(code, erased)
     _check_vs_oracle(k, p, st.cpu().numpy(), got, erased, to_read, ntr, range(S))
     fused = case == "small"
-    assert _run.kernel.startswith("decode_crc_pipe_kernel") == fused, _run.kernel
+    assert _run.kernel.startswith("decode_crc") == fused, _run.kernel
 
 
 @pytest.mark.gpu
