@@ -329,16 +329,21 @@ class _HipErasureCode(ErasureCode):
         """encodeBulk plus Encoder.encodeStripe's block checksums
         (Encoder.java:408-450): returns k + p CRC32 values, sources then
         parities, each continued from `crcs` (CRC32.update chaining across
-        successive cells of a block; None = fresh CRC32 objects)."""
+        successive cells of a block; None = fresh CRC32 objects). Host rows go
+        through the pinned pipeline (hrs_encode_crc), device rows through the
+        fused kernel (hrs_encode_crc_dev; inputs are not zeroed there, as in
+        encodeBulk's device path)."""
         if len(inputs) != self._k or len(outputs) != self._p:
             raise ValueError(f"encodeBulk needs {self._k} inputs and {self._p} outputs")
         ins = _Rows(inputs, writable=False)
         outs = _Rows(outputs, writable=True)
         if ins.len != outs.len:
             raise ValueError("input and output rows differ in length")
-        if self._placement(ins, outs) is not None:
-            raise ValueError("encodeBulkCrc takes host rows (device rows: device.encode_crc_stripes)")
         crc_in, crc_out = self._crc_arrays(crcs, self._k + self._p)
+        dev = self._placement(ins, outs)
+        if dev is not None:  # device rows: one fused pass (hrs_encode_crc_dev)
+            return self._crc_dev(lambda cin, cout, stream: _lib.lib().hrs_encode_crc_dev(
+                self._handle(), ins.ptrs, 0, outs.ptrs, 0, ins.len, 1, cin, cout, stream), dev, crc_in, crc_out.size)
         self._check(_lib.lib().hrs_encode_crc(self._handle(), ins.ptrs, outs.ptrs, ins.len,
                                               None if crc_in is None else crc_in.ctypes.data, crc_out.ctypes.data))
         if self.zero_inputs_after_encode:
@@ -350,7 +355,8 @@ class _HipErasureCode(ErasureCode):
     def decodeBulkCrc(self, readBufs, writeBufs, erasedLocations, locationsToRead, locationsNotToRead, crcs=None):
         """5-arg decodeBulk plus the CRC32 of every repaired buffer, the value
         Decoder compares with the stored block checksum (Decoder.java:222-229,
-        :645-655); continued from `crcs` (None = fresh)."""
+        :645-655); continued from `crcs` (None = fresh). Host rows: hrs_decode_crc;
+        device rows: hrs_decode_crc_dev (one fused pass)."""
         n = self._k + self._p
         if len(readBufs) != n:
             raise ValueError(f"decodeBulk needs {n} read buffers")
@@ -360,11 +366,15 @@ class _HipErasureCode(ErasureCode):
         reads = _Rows([None if (i in ntr and r is None) else r for i, r in enumerate(readBufs)],
                       writable=False, allow_none=True)
         writes = _Rows(writeBufs, writable=True)
-        if self._placement(reads, writes) is not None:
-            raise ValueError("decodeBulkCrc takes host rows")
+        dev = self._placement(reads, writes)
         crc_in, crc_out = self._crc_arrays(crcs, len(erasedLocations))
         if not erasedLocations:
             return []
+        if dev is not None:  # device rows: repair + CRC in one pass (hrs_decode_crc_dev)
+            return self._crc_dev(lambda cin, cout, stream: _lib.lib().hrs_decode_crc_dev(
+                self._handle(), reads.ptrs, 0, writes.ptrs, 0, int_array(erasedLocations), len(erasedLocations),
+                int_array(locationsNotToRead), len(locationsNotToRead), reads.len, 1, cin, cout, stream),
+                dev, crc_in, crc_out.size)
         locationsToRead = locationsToRead or []
         self._check(_lib.lib().hrs_decode_crc(
             self._handle(), reads.ptrs, writes.ptrs, int_array(erasedLocations), len(erasedLocations),
@@ -372,6 +382,18 @@ class _HipErasureCode(ErasureCode):
             len(locationsNotToRead), reads.len, None if crc_in is None else crc_in.ctypes.data,
             crc_out.ctypes.data))
         return [int(x) for x in crc_out]
+
+    def _crc_dev(self, call, dev, crc_in, n):
+        """Runs a device checksum call on the current stream of cuda:dev with
+        device CRC arrays; returns the n CRC32 values (synchronizes)."""
+        torch = _lib.torch
+        out = torch.empty(n, dtype=torch.int32, device=f"cuda:{dev}")
+        cin = None
+        if crc_in is not None:
+            cin = torch.from_numpy(crc_in.view(np.int32).copy()).to(out.device)
+        stream = torch.cuda.current_stream(out.device).cuda_stream
+        self._check(call(None if cin is None else cin.data_ptr(), out.data_ptr(), stream))
+        return [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()]
 
     # -- asynchronous rounds (hrs_*_submit / hrs_collect): round r computes on
     #    the GPU while the caller reads round r + 1; host rows only

@@ -207,3 +207,32 @@ def test_other_codes(cuda):
             got, crc, ref = _run(torch, code, st, erased)
             assert np.array_equal(got, ref), (type(code).__name__, erased)
             _check_crcs(got, crc)
+
+
+@pytest.mark.gpu
+def test_mirror_checksum_methods_take_device_rows(cuda):
+    """HipReedSolomonCode.encodeBulkCrc / decodeBulkCrc with device rows
+    (one stripe, 1-D uint8 tensors) run the fused device calls and agree with
+    the same methods on host rows (the pinned pipeline) and with zlib."""
+    torch = cuda
+    k, p, L = 10, 4, 512 << 10
+    code = HipReedSolomonCode(k, p)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    data = [torch.randint(0, 256, (L,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    par = [torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in range(p)]
+    start = [(0x9E3779B9 * (i + 1)) & 0xFFFFFFFF for i in range(k + p)]
+    crcs = code.encodeBulkCrc(data, par, start)
+    hdata = [d.cpu().numpy() for d in data]
+    hpar = [np.zeros(L, np.uint8) for _ in range(p)]
+    assert crcs == HipReedSolomonCode(k, p, zero_inputs_after_encode=False).encodeBulkCrc(hdata, hpar, start)
+    assert all(np.array_equal(a.cpu().numpy(), b) for a, b in zip(par, hpar))
+    assert crcs == [zlib.crc32(r.tobytes(), s) for r, s in zip(hdata + hpar, start)]
+    stripe = par + data  # hops order: parity first
+    erased = [1, 7]
+    to_read, ntr = _pattern(code, erased)
+    outs = [torch.empty(L, dtype=torch.uint8, device="cuda") for _ in erased]
+    got = code.decodeBulkCrc([stripe[i] if i in to_read else None for i in range(k + p)], outs, erased, to_read, ntr,
+                             [5, 6])
+    assert all(torch.equal(o, stripe[e]) for o, e in zip(outs, erased))
+    assert got == [zlib.crc32(stripe[e].cpu().numpy().tobytes(), s) for e, s in zip(erased, [5, 6])]
