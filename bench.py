@@ -744,6 +744,8 @@ def run(args):
                 "kernel": traffic_key(dfused_kernel) + " + crc_fold_kernel",
                 "fused_ms": stats(dfused_ms),
                 "two_pass_ms": stats(dtwo_ms),
+                "traffic": load_traffic(dfused_kernel),
+                "algorithmic_bytes_per_launch": dec_bytes,
                 "fused_GBps_algorithmic": round(dec_bytes / (float(np.median(dfused_ms)) * 1e-3) / 1e9, 1),
                 "fused_frac": round(dec_bytes / (float(np.median(dfused_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "speedup_vs_two_pass": round(float(np.median(dtwo_ms)) / float(np.median(dfused_ms)), 3),

@@ -116,7 +116,7 @@ def test_fused_config3_cells(cuda):
     erased = [4]
     to_read, ntr = _pattern(code, erased)
     got, crc, ref = _run(torch, code, st, erased)
-    assert _run.kernel == "decode_crc_pipe_kernel<1, 12>"
+    assert _run.kernel.startswith("decode_crc_pipe_kernel<1, 12")
     host = st.cpu().numpy()
     assert np.array_equal(got[:, 0], host[:, 4])  # codewords: the lost cell comes back
     assert np.array_equal(got, ref)
