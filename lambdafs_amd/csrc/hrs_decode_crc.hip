@@ -71,7 +71,7 @@ __device__ __forceinline__ void dc_apply_task(const RowArgs& a, uint64_t t, int 
 // A chain of dependent LDS lookups and cross-lane shuffles (~1,500 cycles),
 // so the kernel issues the NEXT task's loads before it (they would otherwise
 // wait behind it and the wave would keep one window in flight instead of two).
-template <int NOUT>
+template <int NOUT, bool DPP>
 __device__ __forceinline__ void dc_crc_task(const DecodeCrcArgs& d, uint64_t t, int lane, const SliceTab& slices,
                                             const uint32_t* zchunk, const uint32_t* tree,
                                             const uint32_t (&acc)[NOUT][8]) {
@@ -82,37 +82,12 @@ __device__ __forceinline__ void dc_crc_task(const DecodeCrcArgs& d, uint64_t t, 
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
     const uint32_t x = zmul_xor(zchunk, c0[o], c1[o]);
-    const uint32_t c = lane_tree_dpp(tree, x);
+    const uint32_t c = DPP ? lane_tree_dpp(tree, x) : lane_tree(tree, x);
     if (lane == 0) d.raw[(stripe * NOUT + o) * d.r.nwin + w] = c;
   }
 }
 
-// Raw CRCs of two tasks' single output windows together (tasks tA and tB of
-// the 1-output pipelined kernel): their slicing chains and lane trees
-// interleaved level by level, so each dependent LDS lookup / lane move of one
-// tree overlaps the other's.
-__device__ __forceinline__ void dc_crc_pair(const DecodeCrcArgs& d, uint64_t ta, uint64_t tb, int lane,
-                                            const SliceTab& slices, const uint32_t* zchunk, const uint32_t* tree,
-                                            const uint32_t (&acc_a)[1][8], const uint32_t (&acc_b)[1][8]) {
-  uint32_t x[2][8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    x[0][q] = acc_a[0][q];
-    x[1][q] = acc_b[0][q];
-  }
-  uint32_t c0[2], c1[2];
-  rows_piece_crcs<2>(slices, x, c0, c1);
-  uint32_t a = zmul_xor(zchunk, c0[0], c1[0]);
-  uint32_t b = zmul_xor(zchunk, c0[1], c1[1]);
-  lane_tree2_dpp(tree, a, b);
-  if (lane == 0) {
-    const uint64_t sa = ta / d.r.nwin, sb = tb / d.r.nwin;
-    d.raw[sa * d.r.nwin + (ta - sa * d.r.nwin)] = a;  // raw[stripe][0][window]
-    d.raw[sb * d.r.nwin + (tb - sb * d.r.nwin)] = b;
-  }
-}
-
-template <int NOUT, int NINB, bool PAIR>
+template <int NOUT, int NINB, bool DPP>
 __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const DecodeCrcArgs d) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   for (int i = threadIdx.x; i < kCrcLdsWordsA; i += kDecCrcThreads) lds[i] = d.tables[i];
@@ -128,7 +103,7 @@ __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const D
   uint64_t t = wave_id_in_grid();
   if (t >= a.ntasks) return;
   uint32_t ra[NINB][8], rb[NINB][8];
-  uint32_t acc[NOUT][8], acc1[NOUT][8];
+  uint32_t acc[NOUT][8];
   dc_load_task<NOUT, NINB>(a, t, nin, lane, ra);
   uint64_t t1 = t + nwaves;
   if (t1 < a.ntasks) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
@@ -136,29 +111,23 @@ __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const D
     dc_apply_task<NOUT, NINB>(a, t, nin, lane, ra, acc);
     const uint64_t t2 = t1 + nwaves;
     if (t2 < a.ntasks) dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
-    if constexpr (!PAIR) dc_crc_task<NOUT>(d, t, lane, slices, zchunk, tree, acc);
-    if (t1 >= a.ntasks) {
-      if constexpr (PAIR) dc_crc_task<NOUT>(d, t, lane, slices, zchunk, tree, acc);
-      break;
-    }
-    dc_apply_task<NOUT, NINB>(a, t1, nin, lane, rb, acc1);
+    dc_crc_task<NOUT, DPP>(d, t, lane, slices, zchunk, tree, acc);
+    if (t1 >= a.ntasks) break;
+    dc_apply_task<NOUT, NINB>(a, t1, nin, lane, rb, acc);
     const uint64_t t3 = t2 + nwaves;
     if (t3 < a.ntasks) dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
-    if constexpr (PAIR)
-      dc_crc_pair(d, t, t1, lane, slices, zchunk, tree, acc, acc1);
-    else
-      dc_crc_task<NOUT>(d, t1, lane, slices, zchunk, tree, acc1);
+    dc_crc_task<NOUT, DPP>(d, t1, lane, slices, zchunk, tree, acc);
     if (t2 >= a.ntasks) break;
     t = t2;
     t1 = t3;
   }
 }
 
-// HRS_DCRC_PAIR=0 (A/B runs): the 1-output kernel finishes each task's CRC
-// on its own instead of two tasks' CRCs interleaved (dc_crc_pair).
-bool dcrc_pair() {
+// HRS_DCRC_TREE=0 (A/B runs): the lane tree's in-row levels by ds_bpermute
+// (lane_tree) instead of DPP moves (lane_tree_dpp).
+bool dcrc_dpp() {
   static const bool v = [] {
-    const char* e = getenv("HRS_DCRC_PAIR");
+    const char* e = getenv("HRS_DCRC_TREE");
     return !(e && e[0] == '0');
   }();
   return v;
@@ -206,7 +175,7 @@ __global__ void __launch_bounds__(THREADS) decode_crc_kernel(const DecodeCrcArgs
       bitslice(acc[o]);
       store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
     }
-    dc_crc_task<NOUT>(d, t, lane, slices, zchunk, tree, acc);
+    dc_crc_task<NOUT, true>(d, t, lane, slices, zchunk, tree, acc);
   }
 }
 
@@ -238,12 +207,12 @@ hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, d);
     return hipGetLastError();
   } else {
-    auto kern = dcrc_pair() ? decode_crc_pipe_kernel<NOUT, NINB, true> : decode_crc_pipe_kernel<NOUT, NINB, false>;
+    auto kern = dcrc_dpp() ? decode_crc_pipe_kernel<NOUT, NINB, true> : decode_crc_pipe_kernel<NOUT, NINB, false>;
     const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        static_cast<int>(shm));
     if (e != hipSuccess) return e;
-    note_kernel_t("decode_crc_pipe_kernel", NOUT, NINB, dcrc_pair());
+    note_kernel_t("decode_crc_pipe_kernel", NOUT, NINB, dcrc_dpp());
     constexpr uint64_t per_block = kDecCrcThreads / 64;
     uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
     if (g > static_cast<uint64_t>(cus)) g = cus;

@@ -352,22 +352,6 @@ __device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* tree, uint32_t
   return c;
 }
 
-// Two independent lane trees (lane_tree_dpp) advanced level by level.
-__device__ __forceinline__ void lane_tree2_dpp(const uint32_t* tree, uint32_t& a, uint32_t& b) {
-  a = zmul(tree + 0 * 1024, a) ^ dpp_down<1>(a);
-  b = zmul(tree + 0 * 1024, b) ^ dpp_down<1>(b);
-  a = zmul(tree + 1 * 1024, a) ^ dpp_down<2>(a);
-  b = zmul(tree + 1 * 1024, b) ^ dpp_down<2>(b);
-  a = zmul(tree + 2 * 1024, a) ^ dpp_down<4>(a);
-  b = zmul(tree + 2 * 1024, b) ^ dpp_down<4>(b);
-  a = zmul(tree + 3 * 1024, a) ^ dpp_down<8>(a);
-  b = zmul(tree + 3 * 1024, b) ^ dpp_down<8>(b);
-  a = zmul(tree + 4 * 1024, a) ^ __shfl_down(a, 16, 64);
-  b = zmul(tree + 4 * 1024, b) ^ __shfl_down(b, 16, 64);
-  a = zmul(tree + 5 * 1024, a) ^ __shfl_down(a, 32, 64);
-  b = zmul(tree + 5 * 1024, b) ^ __shfl_down(b, 32, 64);
-}
-
 // ---------------------------------------- runtime-matrix kernel helpers
 
 // NINB >= nin rows of the window are all loaded before any math (one
