@@ -4,7 +4,8 @@
 // joins its pieces in chunk order with Z_1024, then a 6-level lane tree with
 // Z_{16*2^t}; the window fold with G windows per lane + Z_{window*G*2^t}
 // tree, the right-aligned tail window and CRC32.update chaining — emulated
-// lane by lane and checked against zlib.
+// lane by lane and checked against zlib; and the fused repair + CRC's 2 KiB
+// windows with its DPP lane tree (hrs_decode_crc.hip).
 #include <zlib.h>
 
 #include <cstdio>
@@ -27,12 +28,17 @@ static std::vector<uint32_t> tab(uint64_t n) {
 static std::vector<uint32_t> zchunk = tab(kChunkBytes);
 static const int64_t W = static_cast<int64_t>(kWindowBytes);
 
+// pieces: chunks of 1 KiB per window (32: the 32 KiB window kernels; 2: the
+// fused repair's 2 KiB task window). dpp: the lane tree's levels 0-3 move
+// within 16-lane rows (DPP row_shl, 0 past the row end) and levels 4-5 keep
+// the lane's own value past lane 63 (__shfl_down), as lane_tree_dpp does;
+// only lane 0's result is used, which never reads a lane past its row.
 static uint32_t window_raw(const Slice4& sl, const std::vector<std::vector<uint32_t>>& tree, const uint8_t* p,
-                           int64_t start, int64_t lo, int64_t end) {
+                           int64_t start, int64_t lo, int64_t end, int pieces = kPieces, bool dpp = false) {
   uint32_t c[64];
   for (int lane = 0; lane < 64; ++lane) {
     uint32_t x = 0;
-    for (int q = 0; q < kPieces; ++q) {
+    for (int q = 0; q < pieces; ++q) {
       uint32_t ch = 0;  // the 16-byte piece at q*1024 + 16*lane
       for (int j = 0; j < 4; ++j) {
         uint32_t w = 0;
@@ -48,11 +54,60 @@ static uint32_t window_raw(const Slice4& sl, const std::vector<std::vector<uint3
     c[lane] = x;
   }
   for (int lvl = 0; lvl < 6; ++lvl) {
+    const int d = 1 << lvl;
     uint32_t n[64];
-    for (int l = 0; l < 64; ++l) n[l] = zmul(tree[lvl], c[l]) ^ (l + (1 << lvl) < 64 ? c[l + (1 << lvl)] : 0);
+    for (int l = 0; l < 64; ++l) {
+      uint32_t o = l + d < 64 ? c[l + d] : 0;
+      if (dpp && lvl < 4 && (l & 15) + d >= 16) o = 0;  // row_shl: nothing from the next row
+      if (dpp && lvl >= 4 && l + d >= 64) o = c[l];     // __shfl_down: own value past the wave
+      n[l] = zmul(tree[lvl], c[l]) ^ o;
+    }
     for (int l = 0; l < 64; ++l) c[l] = n[l];
   }
   return c[0];
+}
+
+// The fused repair + CRC (hrs_decode_crc.hip): raw CRC per 2 KiB window (two
+// pieces per lane, the DPP lane tree), folded like crc_fold_kernel with
+// 2 KiB windows, CRC32.update chaining; lengths are whole windows.
+static int fused_repair_model(const Slice4& sl, const std::vector<std::vector<uint32_t>>& tree, int* cases) {
+  const int64_t W2 = 2048;
+  int bad = 0;
+  uint64_t seed = 7;
+  for (size_t len : {2048ul, 4096ul, 2048ul * 63, 2048ul * 64, 2048ul * 65, 2048ul * 200, 1ul << 20}) {
+    std::vector<uint8_t> d(len);
+    for (auto& x : d) x = (uint8_t)((seed = seed * 6364136223846793005ull + 1442695040888963407ull) >> 56);
+    const uint64_t nwin = len / W2, G = (nwin + 63) / 64;
+    std::vector<uint32_t> raw(nwin);
+    for (uint64_t w = 0; w < nwin; ++w) raw[w] = window_raw(sl, tree, d.data(), w * W2, w * W2, (w + 1) * W2, 2, true);
+    auto zw = tab(W2), zlen = tab(len);
+    std::vector<std::vector<uint32_t>> ft;
+    for (int t = 0; t < 6; ++t) ft.push_back(tab(W2 * G << t));
+    for (uint32_t crc_in : {0u, 0x1234567u}) {
+      uint32_t c[64];
+      const int64_t pad = (int64_t)G * 64 - (int64_t)nwin;
+      for (int l = 0; l < 64; ++l) {
+        c[l] = 0;
+        for (uint64_t g = 0; g < G; ++g) {
+          int64_t w = (int64_t)l * G + g - pad;
+          if (w >= 0) c[l] = zmul(zw, c[l]) ^ raw[w];
+        }
+      }
+      for (int lvl = 0; lvl < 6; ++lvl) {
+        uint32_t n[64];
+        for (int l = 0; l < 64; ++l) n[l] = zmul(ft[lvl], c[l]) ^ (l + (1 << lvl) < 64 ? c[l + (1 << lvl)] : 0);
+        for (int l = 0; l < 64; ++l) c[l] = n[l];
+      }
+      const uint32_t out = zmul(zlen, crc_in ^ 0xFFFFFFFFu) ^ c[0] ^ 0xFFFFFFFFu;
+      const uint32_t ref = (uint32_t)crc32(crc_in, d.data(), (uInt)len);
+      ++*cases;
+      if (out != ref) {
+        ++bad;
+        printf("fused repair window model, len %zu crc_in %08x: model %08x zlib %08x\n", len, crc_in, out, ref);
+      }
+    }
+  }
+  return bad;
 }
 
 int main() {
@@ -99,6 +154,7 @@ int main() {
       }
     }
   }
+  bad += fused_repair_model(sl, tree, &cases);
   printf("{\"crc_model_cases\": %d, \"mismatches\": %d}\n", cases, bad);
   return bad ? 1 : 0;
 }
