@@ -45,12 +45,16 @@ __device__ __forceinline__ void dc_load_task(const RowArgs& a, uint64_t t, int n
 }
 
 // The repair of task t: slice, multiply, un-slice and store its outputs;
-// acc keeps the stored words for dc_crc_task.
+// res receives the stored words for dc_crc_task. The accumulators are local
+// and copied out at the end: accumulated in place through the reference, the
+// 2- and 4-output forms compiled to thousands of v_mov_b64 shuffling them
+// between register pairs at every coefficient branch (NOTES.md, decode_crc/).
 template <int NOUT, int NINB>
 __device__ __forceinline__ void dc_apply_task(const RowArgs& a, uint64_t t, int nin, int lane,
-                                              uint32_t (&rows)[NINB][8], uint32_t (&acc)[NOUT][8]) {
+                                              uint32_t (&rows)[NINB][8], uint32_t (&res)[NOUT][8]) {
   const uint64_t stripe = t / a.nwin;
   const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
+  uint32_t acc[NOUT][8];
 #pragma unroll
   for (int o = 0; o < NOUT; ++o)
 #pragma unroll
@@ -63,6 +67,8 @@ __device__ __forceinline__ void dc_apply_task(const RowArgs& a, uint64_t t, int 
   for (int o = 0; o < NOUT; ++o) {
     bitslice(acc[o]);
     store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) res[o][q] = acc[o][q];
   }
 }
 
