@@ -7,6 +7,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 CC       ?= gcc
 
 LIB      := lambdafs_amd/libhrs.so
+PROBE    := lambdafs_amd/libhrs_probe.so
 ORACLE   := oracle/liboracle.so
 HDRS     := Makefile include/hrs.h lambdafs_amd/csrc/hrs_device.hpp lambdafs_amd/csrc/hrs_launch.hpp lambdafs_amd/csrc/gf256.hpp lambdafs_amd/csrc/hrs_internal.hpp \
             lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp lambdafs_amd/csrc/xor_sched.hpp lambdafs_amd/csrc/hrs_codec.hpp \
@@ -20,7 +21,7 @@ API_OBJ  := $(patsubst %,build/%.o,$(API_SRC))
 JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables
 
-all: $(LIB) $(ORACLE) $(JNI) $(HARNESS)
+all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS)
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build
@@ -57,11 +58,15 @@ build/hrs_probe.o: lambdafs_amd/csrc/hrs_probe.hip include/hrs_probe.h $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_decode_crc.o \
-            build/hrs_probe.o
+KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_decode_crc.o
 
 $(LIB): $(API_OBJ) $(KOBJ) lambdafs_amd/csrc/libhrs.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs.map -o $@ $(API_OBJ) $(KOBJ)
+
+# HBM ceiling probes (include/hrs_probe.h): a side library for bench.py and
+# tools only; the product libhrs.so does not carry diagnostics.
+$(PROBE): build/hrs_probe.o lambdafs_amd/csrc/libhrs_probe.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs_probe.map -o $@ build/hrs_probe.o
 
 $(ORACLE): oracle/rs_oracle.c oracle/rs_oracle.h
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/rs_oracle.c

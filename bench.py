@@ -21,9 +21,17 @@ Run: python bench.py [--gpus N --steps K --warmup W]
      bench.py --gpus N` form runs the ranks directly). A launcher whose
      WORLD_SIZE differs from --gpus is an error.
 
-After timing, the parity and the decoded rows are hashed per block of 256
-global stripes and compared with the C oracle's digests of the same synthetic
-stripes (tests/golden/bench_digests.json); a mismatch fails the run.
+The decode is timed through the decodeBulk boundary itself (hrs_decode_dev:
+the product's argument checks and decode-matrix cache lookup on every call);
+the matrix rank 0 broadcasts over RCCL is a cross-check only.
+
+After timing, every stripe's parity and decoded row get a SHA-256; rank 0
+gets every rank's per-stripe digests and hashes them per block of 256 global
+stripes (tools/stripe_digests.py), so any partition of the stripes over the
+ranks (weak or strong scaling) is compared with the C oracle's digests of the
+same synthetic stripes (tests/golden/bench_digests.json). On a workload the
+oracle covers, a mismatch, a block the oracle has no digest for, or no
+checked block at all fails the run.
 """
 import argparse
 import json
@@ -44,7 +52,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 # Product imports happen in main(), after the launch decision (launch_plan):
 # a relaunching parent must not touch the GPU before it starts its child.
-synth = HipReedSolomonCode = device = parallel = None
+synth = SD = HipReedSolomonCode = device = parallel = None
 
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -202,9 +210,10 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     (hrs_encode_batch_host: 12 data cells H2D, 4 parity cells D2H). The
     repaired cells are hashed per 256-stripe block and compared with the
     oracle's digests (golden["config5"]).
-    Host memory per rank: ~2.3 GiB pinned (stripes + repaired cells) and
-    ~4.3 GiB pageable at peak (the pageable copy, its outputs, one D2H check
-    copy): ~6.5 GiB per rank, ~52 GiB on an 8-GPU node."""
+    Host memory per rank at S = 512: ~2.3 GiB pinned (stripes + repaired
+    cells) and ~2.8 GiB pageable at peak (the pageable copy, its outputs, the
+    check copies), plus the process: e2e_host_bytes(), which run()'s guard
+    (e2e_plan) holds against the host's available memory."""
     k, p = 12, 4
     n = k + p
     code = HipReedSolomonCode(k, p, device=local)
@@ -238,7 +247,7 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     dec_ms = timed(lambda: device.decode_batch_host(code, stn, er, outn))
     idx = np.arange(S)[:, None]
     dec_ok = bool(np.array_equal(outn, stn[idx, er]))
-    mine = block_sha256(lambda a, b: outn[a:b], S, g0)
+    mine = SD.stripe_digests(lambda a, b: outn[a:b], S, g0)
     # pageable host memory: the same call stages through pinned slots
     pg = np.array(stn)
     pout = np.zeros((S, 2, L), np.uint8)
@@ -256,7 +265,7 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     t_enc = parallel.max_over_ranks(float(np.median(enc_ms)), dev)
     t_pg = parallel.max_over_ranks(float(np.median(pg_ms)), dev)
     ok = parallel.all_ok(enc_ok and dec_ok and pg_ok, dev)
-    repaired = gather_blocks(mine, world)
+    repaired = SD.combine(gather_digests(mine))
     user = k * L * S * world
 
     def rate(t_ms, nbytes):
@@ -277,46 +286,26 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
         "encode_GiBps_user": rate(t_enc, user),
         "encode_pcie_GBps": round((k + p) * L * S * world / 1e9 / (t_enc * 1e-3), 2),
         "bit_exact": ok,
-        "repaired_vs_oracle": compare_blocks({"repaired": repaired}, golden.get("config5", {}), ("repaired",)),
+        "repaired_vs_oracle": SD.compare({"repaired": repaired}, golden.get("config5", {}), ("repaired",),
+                                         golden.get("config5", {}).get("stripes", 0)),
+        "stripes_per_gpu": S,
         "n_gpus": world,
     }
 
 
-def block_sha256(rows_of, S, g0, block=256):
-    """SHA-256 per block of `block` consecutive GLOBAL stripes (a block starts
-    at a multiple of `block`) of this rank's stripes g0 .. g0+S-1; rows_of(a, b)
-    returns the bytes to hash for local stripes [a, b) (a tensor, device or
-    host, or an array), hashed stripe by stripe in order. {block key: digest},
-    key "g" for a whole block, "g+n" for a partial one. Inputs are keyed by
-    global stripe index, so any N-GPU run covering a block prints the same
-    digest for it, and tests/golden/bench_digests.json holds the oracle's."""
-    import hashlib
-    out = {}
-    s = 0
-    while s < S:
-        g = g0 + s
-        nb = min(block - g % block, S - s)
-        h = hashlib.sha256()
-        for s0 in range(s, s + nb, 64):
-            x = rows_of(s0, min(s + nb, s0 + 64))
-            if isinstance(x, torch.Tensor):
-                x = x.contiguous().cpu().numpy()
-            h.update(np.ascontiguousarray(x).tobytes())
-        out[f"{g}" if nb == block else f"{g}+{nb}"] = h.hexdigest()
-        s += nb
-    return out
-
-
-def gather_blocks(mine, world):
-    """Union of every rank's block digests (all_gather_object)."""
-    allv = [mine]
-    if dist.is_available() and dist.is_initialized():
-        allv = [None] * world
-        dist.all_gather_object(allv, mine)
+def gather_digests(mine):
+    """Union of every rank's per-stripe digests ({global stripe: digest}),
+    on every rank."""
     merged = {}
-    for d in allv:
+    for d in parallel.gather_objects(mine):
         merged.update(d)
-    return dict(sorted(merged.items(), key=lambda kv: int(kv[0].split("+")[0])))
+    return merged
+
+
+def oracle_blocks(rows_of, S, g0):
+    """Block digests of this job's outputs: each rank hashes its own stripes,
+    every rank assembles the union (tools/stripe_digests.py)."""
+    return SD.combine(gather_digests(SD.stripe_digests(rows_of, S, g0)))
 
 
 def load_golden():
@@ -328,29 +317,79 @@ def load_golden():
         return {}
 
 
-def compare_blocks(got, want, fields):
-    """Compares printed block digests with the oracle's. Returns None when no
-    block of this run is in the golden file (another workload shape), else
-    {"blocks": n, "match": True}; raises on any mismatch."""
-    n = 0
-    for f in fields:
-        ref = want.get(f, {})
-        for key, dig in got[f].items():
-            if key not in ref:
-                continue
-            if ref[key] != dig:
-                raise RuntimeError(f"{f} block {key}: digest {dig} != oracle {ref[key]}")
-            n += 1
-    return {"blocks": n, "match": True} if n else None
+def host_available_bytes():
+    """Host memory this process can still use: MemAvailable, capped by the
+    cgroup v2 limit less its current usage when a limit is set (the GPU boxes
+    give each job a share of a larger machine). None if neither is readable."""
+    vals = []
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    vals.append(int(line.split()[1]) * 1024)
+    except (OSError, ValueError, IndexError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/memory.max") as f:
+            lim = f.read().strip()
+        if lim != "max":
+            with open("/sys/fs/cgroup/memory.current") as f:
+                vals.append(int(lim) - int(f.read().strip()))
+    except (OSError, ValueError):
+        pass
+    return min(vals) if vals else None
+
+
+E2E_BASE_BYTES = 3 << 29  # per rank besides the stripes: torch, HIP runtime, pinned slot staging
+
+
+def e2e_host_bytes(S, L=256 << 10, n=16, e=2):
+    """Peak host bytes of one rank's config-5 leg (e2e_config5): the pinned
+    stripes and repaired cells, then the pageable copy, its outputs and the
+    two fancy-indexed check copies, alive together."""
+    return (2 * n + 3 * e) * L * S + E2E_BASE_BYTES
+
+
+def e2e_plan(avail, local_ranks, S=512):
+    """Stripes per rank for the config-5 leg under the host-memory guard:
+    S, or S/2 (down to one 256-stripe oracle block, so the repaired cells stay
+    checkable), if every rank on this host fits in 3/4 of what is available;
+    else 0 and the reason. `avail` None (unknown) runs the full leg."""
+    if avail is None:
+        return S, None
+    s = S
+    while s >= 256:
+        if local_ranks * e2e_host_bytes(s) <= 0.75 * avail:
+            return s, (None if s == S else f"host memory: {avail / GiB:.1f} GiB available for {local_ranks} "
+                                           f"rank(s) on this host; {s} stripes per rank instead of {S}")
+        s //= 2
+    return 0, (f"skipped: {local_ranks} rank(s) x {e2e_host_bytes(256) / GiB:.1f} GiB for the smallest checkable "
+               f"leg exceed 3/4 of the {avail / GiB:.1f} GiB of host memory available")
+
+
+# hrs_probe_stream shapes swept for the copy / read / write ceilings:
+# (schedule, depth, nontemporal, block threads, blocks per CU). The first is
+# the fastest copy of tools/copy_lab.hip's 252-variant sweep on this pool
+# (block ranges: each 1024-thread block streams its own contiguous 1/256 of the
+# buffer, 8 loads per thread in flight; profiles/r04/copy_lab/), then the
+# runner-ups of other schedules, and the grid-stride float4 loop of the
+# guide's STREAM figure (MI355X_MICROARCH.md: 6.29 TB/s).
+PROBE_SHAPES = (
+    ("block8_nt_1024x1", 2, 8, True, 1024, 1),
+    ("block8_plain_1024x1", 2, 8, False, 1024, 1),
+    ("block4_plain_1024x1", 2, 4, False, 1024, 1),
+    ("wave4K_plain_256x1", 0, 4, False, 256, 1),
+    ("wave1K_nt_256x4", 0, 1, True, 256, 4),
+    ("grid4_nt_256x1", 1, 4, True, 256, 1),
+    ("grid1_nt_256x4", 1, 1, True, 256, 4),
+    ("grid1_plain_1024x1", 1, 1, False, 1024, 1),
+)
 
 
 def hbm_probes(dev, stripes=None, patterns=(), nbytes=4 << 30, reps=5):
-    """This GPU's streaming ceilings, measured in this run by the engine's
-    probes (include/hrs_probe.h), median of `reps` launches each; every
-    figure is the fastest of a small sweep of shapes (wave-task chunk of 1 or
-    8 contiguous KiB, nontemporal or default policy, 1/2/4 blocks of 256
-    threads per CU; round 1's lab found the best shape differs per stream,
-    profiles/r01/lab8_bw_ceilings.txt):
+    """This GPU's streaming ceilings, measured in this run by the probes of
+    libhrs_probe.so (include/hrs_probe.h), median of `reps` launches each;
+    every figure is the fastest of the PROBE_SHAPES sweep:
       copy    : 4 GiB read + 4 GiB written (hrs_probe_stream COPY, and
                 torch's D2D copy_) — SURVEY §8d's "device-copy STREAM peak";
       read    : read-only stream of 4 GiB;
@@ -388,32 +427,35 @@ def hbm_probes(dev, stripes=None, patterns=(), nbytes=4 << 30, reps=5):
     def rate(moved, fn):
         return round(moved / (timed(fn) * 1e-3) / 1e9, 1)
 
-    shapes = [(c, nt, bpc) for c in (1, 8) for nt in (True, False) for bpc in (1, 2, 4)]
-    tag = lambda c, nt, bpc: f"{c}K_{'nt' if nt else 'plain'}_{bpc}cu"
+    def kw(shape):
+        _, sc, d, nt, blk, bpc = shape
+        return dict(schedule=sc, depth=d, nontemporal=nt, block_threads=blk, blocks_per_cu=bpc)
+
     copies = {}
-    for c, nt, bpc in shapes:
-        copies[tag(c, nt, bpc)] = rate(2 * nbytes, lambda: device.probe_copy(src, dst, bpc, c, nt))
+    for shape in PROBE_SHAPES:
+        copies[shape[0]] = rate(2 * nbytes, lambda: device.probe_copy(src, dst, **kw(shape)))
         if not torch.equal(dst[::97], src[::97]):
-            raise RuntimeError(f"copy probe {tag(c, nt, bpc)} mismatch")
+            raise RuntimeError(f"copy probe {shape[0]} mismatch")
         dst.zero_()
     copies["torch_copy"] = rate(2 * nbytes, lambda: dst.copy_(src))
-    reads = {tag(c, True, bpc): rate(nbytes, lambda: device.probe_read(src, sink, bpc, c, True))
-             for c in (1, 8) for bpc in (1, 2, 4)}
-    writes = {tag(c, nt, bpc): rate(nbytes, lambda: device.probe_write(dst, bpc, c, nt)) for c, nt, bpc in shapes}
-    if int(sink.sum().item()) != 0 or dst[0, 4:8].tolist() != [0x5A] * 4:  # element 0 = (t, 0x5A5A5A5A, ..)
+    reads = {sh[0]: rate(nbytes, lambda: device.probe_read(src, sink, **kw(sh))) for sh in PROBE_SHAPES}
+    writes = {sh[0]: rate(nbytes, lambda: device.probe_write(dst, **kw(sh))) for sh in PROBE_SHAPES}
+    if int(sink.sum().item()) != 0 or dst[0, 4:8].tolist() != [0x5A] * 4:  # element 0 = (0, 0x5A5A5A5A, ..)
         raise RuntimeError("read / write probes did not run as intended")
     del src, dst, sink
     torch.cuda.empty_cache()
     best = lambda d: max(d, key=d.get)
     out = {
         "copy": {"GBps": copies[best(copies)], "best": best(copies), "variants": copies,
-                 "how": "4 GiB D2D (bytes read + written), hrs_probe_stream COPY over the shape sweep and torch "
-                        "copy_; GBps = the fastest"},
+                 "guide_copy_GBps": 6290.0,
+                 "how": "4 GiB D2D (bytes read + written), hrs_probe_stream COPY over PROBE_SHAPES and torch "
+                        "copy_; GBps = the fastest. guide_copy_GBps: MI355X_MICROARCH.md's float4 copy figure "
+                        "(box-to-box spread on this pool: DESIGN.md §5)"},
         "read_GBps": reads[best(reads)], "read_best": best(reads),
         "write_GBps": writes[best(writes)], "write_best": best(writes),
         "read_variants": reads, "write_variants": writes,
-        "how": "hrs_probe_stream READ / WRITE over 4 GiB, fastest of the shape sweep (task chunk KiB, policy, "
-               "blocks per CU), median of 5 launches each",
+        "how": "hrs_probe_stream READ / WRITE over 4 GiB, fastest of PROBE_SHAPES (schedule, depth, policy, "
+               "block size, blocks per CU), median of 5 launches each",
         "pattern": {},
     }
     if stripes is not None:
@@ -461,17 +503,26 @@ def traffic_key(name):
     return m.group(1).replace(", ", ",") if m else name
 
 
-def load_traffic(kernel):
+def load_traffic(kernel, workload):
     """PMC HBM bytes per launch of `kernel` (the name the run launched) from
-    profiles/pmc_traffic.json; raises if the kernel has no entry, so a kernel
-    change cannot silently print stale or missing traffic."""
+    profiles/pmc_traffic.json, measured on the workload its "_workload" entry
+    names. Returns (bytes, None), or (None, reason) when the kernel has no
+    entry or this run's workload (k, p, cell, stripes per launch) is not the
+    profiled one — never a stale or rescaled figure, and never an exception
+    on one rank while the others wait in a collective."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    with open(path) as f:
-        table = json.load(f)
+    try:
+        with open(path) as f:
+            table = json.load(f)
+    except (OSError, ValueError) as e:
+        return None, f"cannot read {path}: {e}"
     key = traffic_key(kernel)
+    prof = table.get("_workload")
+    if prof != workload:
+        return None, f"PMC passes were taken on {prof}, this run is {workload}"
     if key not in table:
-        raise RuntimeError(f"no PMC traffic for kernel {key} in {path}: profile it (profiles/run_rocprof.sh)")
-    return table[key]
+        return None, f"no PMC pass for kernel {key} (profiles/run_rocprof.sh)"
+    return table[key], None
 
 
 def main():
@@ -493,10 +544,11 @@ def main():
 
 
 def run(args):
-    global synth, HipReedSolomonCode, device, parallel
+    global synth, SD, HipReedSolomonCode, device, parallel
     import synth as _synth  # SURVEY §8(d) synthetic stripes: splitmix64 per global stripe
+    import stripe_digests as _SD  # per-stripe digests, combined per 256-stripe block
     from lambdafs_amd import HipReedSolomonCode as _Code, device as _device, parallel as _parallel
-    synth, HipReedSolomonCode, device, parallel = _synth, _Code, _device, _parallel
+    synth, SD, HipReedSolomonCode, device, parallel = _synth, _SD, _Code, _device, _parallel
 
     world, rank, local = setup_dist(args)
     k, p, L = args.k, args.p, args.cell
@@ -509,8 +561,15 @@ def run(args):
     dev = f"cuda:{local}"
     code = HipReedSolomonCode(k, p, device=local)
     golden = load_golden()
+    # the config-5 leg's host-memory guard, decided before any large allocation
+    # and agreed over the ranks (every rank runs the leg with the same S, or none)
+    local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    e2e_S, e2e_why = (0, "skipped: --no-e2e") if args.no_e2e else e2e_plan(host_available_bytes(), local_ranks)
+    e2e_S = parallel.min_over_ranks(e2e_S, dev)
 
     # coding matrices: built on rank 0, broadcast over RCCL, checked everywhere
+    # (the timed decode goes through hrs_decode_dev; the broadcast D is the
+    # cross-check of its output below)
     erased = [p]  # data shard 0 = hops location p
     to_read = sorted(code.locationsToReadForDecode(erased))
     ntr = [x for x in range(n) if x not in to_read]
@@ -526,16 +585,15 @@ def run(args):
     synth.fill_data_rows(torch, stripes, 3, g0, k, p)
     out = torch.empty((S, len(erased), L), dtype=torch.uint8, device=dev)
     in_rows = [stripes[:, loc, :] for loc in to_read]
-    out_rows = [out[:, 0, :]]
     assert G.shape == (p, k)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record()
-        device.encode_stripes(code, stripes)
+        device.encode_stripes(code, stripes)  # encodeBulk over S stripes (hrs_encode_dev)
         if ev is not None:
             ev[1].record()
-        device.apply_rows(code, D_live, in_rows, out_rows)
+        device.decode_stripes(code, stripes, erased, ntr, out)  # decodeBulk 5-arg (hrs_decode_dev)
         if ev is not None:
             ev[2].record()
 
@@ -549,9 +607,10 @@ def run(args):
     for i in range(args.steps):
         step(events[i])
     torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
     parallel.barrier()
-    elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
-    dec_kernel = code.lastKernel()  # the decode step's kernel (apply_rows ran last)
+    elapsed = parallel.max_over_ranks(wall, dev)
+    dec_kernel = code.lastKernel()  # the decode step's kernel (decode_stripes ran last)
     device.encode_stripes(code, stripes)  # idempotent: same parity; names the encode kernel
     enc_kernel = code.lastKernel()
     torch.cuda.synchronize()
@@ -560,11 +619,21 @@ def run(args):
     dec_all = [e[1].elapsed_time(e[2]) for e in events]
     enc_ms = float(np.mean(enc_all))
     dec_ms = float(np.mean(dec_all))
+    # per-rank evidence for the scaling line: which rank or phase lagged
+    per_rank = parallel.gather_objects({
+        "rank": rank, "local_rank": local, "host": socket.gethostname(), "g0": g0, "stripes": S,
+        "wall_s": round(wall, 6), "encode_ms": stats(enc_all), "decode_ms": stats(dec_all),
+        "encode_kernel": traffic_key(enc_kernel), "decode_kernel": traffic_key(dec_kernel)})
 
-    # correctness of what was timed: the decode must reproduce data shard 0
+    # correctness of what was timed: the decode must reproduce data shard 0,
+    # and equal the broadcast matrix applied to the same survivors
     ok = bool(torch.equal(out[:, 0], stripes[:, p]))
     ok &= bool(torch.equal(stripes[min(S - 1, S // 2), p:].cpu(),
                            torch.from_numpy(synth.stripe_numpy(3, g0 + min(S - 1, S // 2), k, L))))
+    xcheck = torch.empty_like(out)
+    device.apply_rows(code, D_live, in_rows, [xcheck[:, 0, :]])
+    ok &= bool(torch.equal(xcheck, out))
+    del xcheck
     if args.check:
         from oracle import rs_oracle as C
         for s_chk in sorted({0, S // 2, S - 1}):
@@ -633,28 +702,38 @@ def run(args):
     if not parallel.all_ok(bool(torch.equal(out_crc, out)) and bool(torch.equal(dcrc_fused, dcrc_two)), dev):
         raise RuntimeError("fused decode+CRC differs from decode then CRC")
     dfused_ms = med_ms(lambda: device.decode_stripes_crc(code, stripes, erased, ntr, out_crc), reps)
-    dtwo_ms = med_ms(lambda: (device.apply_rows(code, D_live, in_rows, out_rows),
+    dtwo_ms = med_ms(lambda: (device.decode_stripes(code, stripes, erased, ntr, out),
                               device.crc32_rows(code, [out[:, 0, :]])), reps)
     del out_crc
 
-    # the timed outputs against the oracle: parity and decoded rows per block
-    # of 256 global stripes vs tests/golden/bench_digests.json
+    # the timed outputs against the oracle: every stripe's parity and decoded
+    # row hashed on its rank, the union hashed per block of 256 global stripes
+    # and compared with tests/golden/bench_digests.json (SD.compare raises on
+    # a mismatch, on a block the oracle cannot check, and on no block checked
+    # — on every rank alike, since every rank holds the union)
     sha = None
-    vs_oracle = None
-    if not args.no_sha:
-        digs = {"parity": gather_blocks(block_sha256(lambda a, b: stripes[a:b, :p], S, g0), world),
-                "decode": gather_blocks(block_sha256(lambda a, b: out[a:b], S, g0), world)}
-        sha = {"block_stripes": 256, "blocks": digs["parity"], "decode_blocks": digs["decode"]}
-        want = golden.get("config3", {})
-        if (k, p, L) == (want.get("k"), want.get("p"), want.get("cell")):
-            vs_oracle = compare_blocks(digs, want, ("parity", "decode"))
-    e2e = None
-    if not args.no_e2e:
+    want = golden.get("config3", {})
+    golden_workload = (k, p, L) == (want.get("k"), want.get("p"), want.get("cell"))
+    if args.no_sha:
+        vs_oracle = {"skipped": "--no-sha"}
+    else:
+        digs = {"parity": oracle_blocks(lambda a, b: stripes[a:b, :p], S, g0),
+                "decode": oracle_blocks(lambda a, b: out[a:b], S, g0)}
+        sha = {"block_stripes": SD.BLOCK, "scheme": "sha256 of the per-stripe sha256 digests in global order",
+               "blocks": digs["parity"], "decode_blocks": digs["decode"]}
+        if golden_workload:
+            vs_oracle = SD.compare(digs, want, ("parity", "decode"), want.get("stripes", 8 * 1024))
+        else:
+            vs_oracle = {"skipped": f"no oracle digests for RS({k},{p}) x {L} B cells"}
+    e2e = {"skipped": e2e_why} if e2e_S == 0 else None
+    if e2e_S:
         del cells
         torch.cuda.empty_cache()
-        e2e = e2e_config5(local, rank, world, golden)
-        if e2e["repaired_vs_oracle"] is None:
-            raise RuntimeError("config 5 repaired cells: no oracle digest to compare with")
+        e2e = e2e_config5(local, rank, world, golden, S=e2e_S)
+        if e2e_why:
+            e2e["memory_guard"] = e2e_why
+        if not e2e["bit_exact"]:
+            raise RuntimeError("config 5 end-to-end leg: outputs differ from the device-resident ones")
 
     total_stripes = args.stripes if args.strong else S * world
     user_bytes = 2 * k * L * total_stripes * args.steps
@@ -668,6 +747,11 @@ def run(args):
     if rank == 0:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             traffic_note = json.load(f).get("_note")
+        wl = {"k": k, "p": p, "cell": L, "stripes": S}
+        enc_traffic, enc_traffic_why = load_traffic(enc_kernel, wl)
+        dec_traffic, dec_traffic_why = load_traffic(dec_kernel, wl)
+        rand_traffic, rand_traffic_why = load_traffic(batch_kernel, wl)
+        dcrc_traffic, dcrc_traffic_why = load_traffic(dfused_kernel, wl)
         res = {
             "metric": "RS encode+decode GiB/s device-resident; 1/2/4/8 MI355X; %HBM roofline",
             "value": round(user_bytes / GiB / elapsed, 3),
@@ -684,7 +768,8 @@ def run(args):
                     "0x00/0xFF/ramp at global 0..2 (SURVEY §8d)",
             "config": {
                 "workload": f"RS({k},{p}) encode + 1-erasure decode (data shard 0), {L >> 10} KiB cells, "
-                            f"{S} stripes/GPU, device-resident",
+                            f"{S} stripes/GPU, device-resident; encodeBulk / decodeBulk via hrs_encode_dev / "
+                            "hrs_decode_dev",
                 "stripes_per_gpu": S, "stripes_total": total_stripes, "cell_bytes": L, "k": k, "p": p,
                 "parallelism": f"stripe-sharded x{world} (RCCL: matrix broadcast + barriers only)",
                 "collectives": (dist.get_backend() if dist.is_available() and dist.is_initialized() else None),
@@ -692,6 +777,7 @@ def run(args):
             "parity_vs_oracle": vs_oracle,
             "encode_GiBps_per_gpu": round(k * L * S / GiB / (enc_ms * 1e-3), 3),
             "decode_GiBps_per_gpu": round(k * L * S / GiB / (dec_ms * 1e-3), 3),
+            "per_rank": per_rank,
             "roofline": {
                 "kernel": traffic_key(enc_kernel),
                 "bound": "hbm",
@@ -699,8 +785,8 @@ def run(args):
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic(enc_kernel),
-                "traffic_source": traffic_note,
+                "traffic": enc_traffic,
+                "traffic_source": traffic_note if enc_traffic is not None else enc_traffic_why,
                 "avg_launch_ms": round(enc_ms, 4),
                 "launch_ms": stats(enc_all),
                 "algorithmic_bytes_per_launch": enc_bytes,
@@ -711,13 +797,15 @@ def run(args):
                 **pattern_fields(probes, "encode", enc_gbps),
             },
             "decode_roofline": {
-                "kernel": traffic_key(dec_kernel), "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
+                "kernel": traffic_key(dec_kernel), "entry_point": "hrs_decode_dev",
+                "achieved": round(dec_gbps, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(dec_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(dec_ms, 4),
                 "launch_ms": stats(dec_all), "frac_vs_copy": round(dec_gbps / probes["copy"]["GBps"], 4),
                 "mix_ceiling": round(mix_ceiling(probes, k, len(erased)), 1),
                 "frac_vs_mix_ceiling": round(dec_gbps / mix_ceiling(probes, k, len(erased)), 4),
                 **pattern_fields(probes, "decode", dec_gbps),
-                "traffic": load_traffic(dec_kernel),
+                "traffic": dec_traffic,
+                "traffic_source": traffic_note if dec_traffic is not None else dec_traffic_why,
                 "algorithmic_bytes_per_launch": dec_bytes,
             },
             "random_location_decode": {
@@ -727,7 +815,8 @@ def run(args):
                 "kernel": traffic_key(batch_kernel),
                 "GBps_algorithmic": round((k + 1) * L * S / (float(np.median(rand_ms)) * 1e-3) / 1e9, 1),
                 "algorithmic_bytes_per_launch": (k + 1) * L * S,
-                "traffic": load_traffic(batch_kernel),
+                "traffic": rand_traffic,
+                "traffic_source": None if rand_traffic is not None else rand_traffic_why,
                 "GiBps_user_per_gpu": round(k * L * S / GiB / (float(np.median(rand_ms)) * 1e-3), 3),
             },
             "encode_crc": {
@@ -744,7 +833,8 @@ def run(args):
                 "kernel": traffic_key(dfused_kernel) + " + crc_fold_kernel",
                 "fused_ms": stats(dfused_ms),
                 "two_pass_ms": stats(dtwo_ms),
-                "traffic": load_traffic(dfused_kernel),
+                "traffic": dcrc_traffic,
+                "traffic_source": None if dcrc_traffic is not None else dcrc_traffic_why,
                 "algorithmic_bytes_per_launch": dec_bytes,
                 "fused_GBps_algorithmic": round(dec_bytes / (float(np.median(dfused_ms)) * 1e-3) / 1e9, 1),
                 "fused_frac": round(dec_bytes / (float(np.median(dfused_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),

@@ -1,23 +1,21 @@
 /*
- * hrs_probe.h — HBM ceiling probes exported by libhrs.so (diagnostic; not part
- * of the codec plugin surface, so they have no reference counterpart).
+ * hrs_probe.h — HBM ceiling probes, exported by libhrs_probe.so: a side
+ * library that bench.py and tools load. The product library (libhrs.so, the
+ * one a DataNode JVM loads) does not carry them; they have no reference
+ * counterpart.
  *
  * bench.py quotes the coding kernels' bandwidth against the nominal 8 TB/s
  * and against what this GPU streams in the same run ("a
  * measured device-copy STREAM peak"):
- *   - hrs_probe_stream: copy, read-only and write-only streams in the shapes
- *     of round 1's bandwidth lab (profiles/r01/lab8_bw_ceilings.txt): a wave
- *     task is `chunk_kib` KiB contiguous, one 16-byte access per lane per KiB,
- *     the task's loads all issued before any is used; nontemporal or default
- *     policy; bench.py takes the fastest of a small sweep of shapes.
+ *   - hrs_probe_stream: copy, read-only and write-only streams under three
+ *     schedules (tools/copy_lab.hip, profiles/r04/copy_lab/); bench.py takes
+ *     the fastest of a small sweep;
  *   - hrs_probe_rows: the coding kernels' own access pattern with the GF math
  *     taken out. A 1:1 copy is not a ceiling for the codec's read-heavy mixes
  *     (RS(10,4) encode reads 10 rows per 4 written, a repair 10 per 1), and
  *     neither is the mix of the read-only and write-only peaks, because HBM
  *     pays for turning its bus between reads and writes; this probe moves the
  *     same bytes in the same order, so it is the ceiling of the pattern.
- * hrs_probe_copy / _read / _write are the 1 KiB-task nontemporal streams
- * (= a grid-stride loop over 16-byte elements).
  */
 #ifndef HRS_PROBE_H_
 #define HRS_PROBE_H_
@@ -31,29 +29,27 @@ extern "C" {
 #endif
 
 enum { HRS_PROBE_COPY = 0, HRS_PROBE_READ = 1, HRS_PROBE_WRITE = 2 };
+enum { HRS_PROBE_WAVE_TASKS = 0, HRS_PROBE_GRID_STRIDE = 1, HRS_PROBE_BLOCK_RANGE = 2 };
 
-/* One streaming pass on `stream` (a hipStream_t; NULL = null stream),
- * asynchronous:
+/* One streaming pass over `bytes` on `stream` (a hipStream_t; NULL = null
+ * stream), asynchronous:
  *   HRS_PROBE_COPY  dst[0, bytes) = src[0, bytes);
  *   HRS_PROBE_READ  reads src[0, bytes) once; `dst` is a device sink of
- *                   >= 4 KiB, written only in a case that cannot occur (it
- *                   keeps the loads alive);
+ *                   >= 4 KiB, written only if the data XOR to one particular
+ *                   value (it keeps the loads alive);
  *   HRS_PROBE_WRITE writes dst[0, bytes) once (src unused, may be NULL).
- * chunk_kib in {1, 2, 4, 8}: contiguous KiB per wave task; nontemporal != 0
- * uses nontemporal loads / stores; the grid is blocks_per_cu (1..32) x the
- * current device's CUs of 256 threads. Pointers and bytes must be multiples
- * of 16 (else HRS_EALIGN); other bad arguments HRS_EINVAL. */
-hrs_status hrs_probe_stream(int op, const void* src, void* dst, size_t bytes, int chunk_kib, int nontemporal,
-                            int blocks_per_cu, void* stream);
-
-/* = hrs_probe_stream(HRS_PROBE_COPY, src, dst, bytes, 1, 1, blocks_per_cu, stream). */
-hrs_status hrs_probe_copy(const void* src, void* dst, size_t bytes, int blocks_per_cu, void* stream);
-
-/* = hrs_probe_stream(HRS_PROBE_READ, src, sink, bytes, 1, 1, blocks_per_cu, stream). */
-hrs_status hrs_probe_read(const void* src, size_t bytes, int blocks_per_cu, void* sink, void* stream);
-
-/* = hrs_probe_stream(HRS_PROBE_WRITE, NULL, dst, bytes, 1, 1, blocks_per_cu, stream). */
-hrs_status hrs_probe_write(void* dst, size_t bytes, int blocks_per_cu, void* stream);
+ * schedule: HRS_PROBE_WAVE_TASKS — a wave task is `depth` contiguous KiB;
+ * HRS_PROBE_GRID_STRIDE — thread i moves 16-byte elements i + j * (grid
+ * threads), `depth` in flight; HRS_PROBE_BLOCK_RANGE — each block streams its
+ * own contiguous 1/grid of the buffer, block-stride, `depth` elements per
+ * thread in flight. depth in {1, 2, 4, 8}; in every schedule a thread issues
+ * all `depth` loads before it uses one. nontemporal != 0 uses nontemporal
+ * loads / stores. The grid is blocks_per_cu x the current device's CUs of
+ * block_threads (256, 512 or 1024) threads, blocks_per_cu * block_threads <=
+ * 8192. Pointers and bytes must be multiples of 16 (else HRS_EALIGN); other
+ * bad arguments HRS_EINVAL. */
+hrs_status hrs_probe_stream(int op, const void* src, void* dst, size_t bytes, int schedule, int depth,
+                            int nontemporal, int block_threads, int blocks_per_cu, void* stream);
 
 /* The coding kernels' access pattern without the math, over `nstripes`
  * stripes of `nrows` rows of `cell_bytes` each, stripe-major and contiguous

@@ -14,6 +14,8 @@ except ImportError:  # pragma: no cover
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HRS_LIB") or os.path.join(_HERE, "libhrs.so")  # HRS_LIB: A/B runs of another build
+# HBM ceiling probes: a side library for bench.py and tools, not the product
+PROBE_LIB_PATH = os.path.join(_HERE, "libhrs_probe.so")
 
 HRS_OK = 0
 HRS_EINVAL = 1
@@ -27,8 +29,8 @@ HRS_CODE_XOR = 1
 HRS_CODE_NRS = 2
 HRS_CODE_SRC = 3
 
-# Every entry point declared in include/hrs.h and include/hrs_probe.h
-# (checked by tests/test_abi.py).
+# Every entry point declared in include/hrs.h (checked by tests/test_abi.py:
+# libhrs.so exports exactly these).
 EXPORTS = (
     "hrs_create", "hrs_create_code", "hrs_create_src", "hrs_src_layout", "hrs_code_kind", "hrs_destroy",
     "hrs_last_error", "hrs_version", "hrs_locations_to_read_list",
@@ -38,9 +40,10 @@ EXPORTS = (
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
     "hrs_encode_crc_dev", "hrs_decode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
-    "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_probe_copy", "hrs_probe_read", "hrs_probe_write", "hrs_wait",
-    "hrs_probe_stream", "hrs_probe_rows",
+    "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_wait",
 )
+# include/hrs_probe.h, exported by libhrs_probe.so
+PROBE_EXPORTS = ("hrs_probe_stream", "hrs_probe_rows")
 
 
 class HrsError(IOError):
@@ -109,17 +112,33 @@ def lib():
         "hrs_ticket_shape": ([P, ctypes.c_uint64, IP, ctypes.POINTER(ctypes.c_size_t), IP], I),
         "hrs_set_kernel_mode": ([P, I], I),
         "hrs_last_kernel": ([P], ctypes.c_char_p),
-        "hrs_probe_copy": ([P, P, S, I, P], I),
-        "hrs_probe_read": ([P, S, I, P, P], I),
-        "hrs_probe_write": ([P, S, I, P], I),
-        "hrs_probe_stream": ([I, P, P, S, I, I, I, P], I),
-        "hrs_probe_rows": ([P, S, I, S, I, I, I, I, P], I),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
     _lib = L
+    return L
+
+
+_probe = None
+
+
+def probe_lib():
+    """Load libhrs_probe.so (include/hrs_probe.h: the HBM ceiling probes
+    bench.py quotes beside the kernels)."""
+    global _probe
+    if _probe is not None:
+        return _probe
+    if not os.path.exists(PROBE_LIB_PATH):
+        raise ImportError(f"{PROBE_LIB_PATH} is missing: build it first (make)")
+    L = ctypes.CDLL(PROBE_LIB_PATH)
+    I, S, P = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+    L.hrs_probe_stream.argtypes = [I, P, P, S, I, I, I, I, I, P]
+    L.hrs_probe_stream.restype = I
+    L.hrs_probe_rows.argtypes = [P, S, I, S, I, I, I, I, P]
+    L.hrs_probe_rows.restype = I
+    _probe = L
     return L
 
 

@@ -189,15 +189,20 @@ void hrs_destroy(hrs_codec* c) {
     if (a.dev) (void)hipFree(a.dev);
     if (a.pin) (void)hipHostFree(a.pin);
   }
+  for (hipStream_t s : {c->hbatch_in, c->hbatch_out})
+    if (s) (void)hipStreamSynchronize(s);
   for (auto& h : c->hbatch) {
     if (h.stream) {
       (void)hipStreamSynchronize(h.stream);
       (void)hipStreamDestroy(h.stream);
     }
-    if (h.done) (void)hipEventDestroy(h.done);
+    for (hipEvent_t e : {h.done, h.in_done, h.comp_done})
+      if (e) (void)hipEventDestroy(e);
     if (h.dev) (void)hipFree(h.dev);
     if (h.pin) (void)hipHostFree(h.pin);
   }
+  for (hipStream_t s : {c->hbatch_in, c->hbatch_out})
+    if (s) (void)hipStreamDestroy(s);
   for (auto& b : c->batch) {
     if (b.done) {
       (void)hipEventSynchronize(b.done);

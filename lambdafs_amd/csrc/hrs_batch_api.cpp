@@ -186,8 +186,10 @@ hrs_status upload_batch_plans(hrs_codec* c, const BatchPlanSet& ps, hipStream_t 
 // ------------------------------------------------ host-memory batches
 // (hrs_decode_batch_host / hrs_encode_batch_host). Stripes start and end in
 // host memory (DataNode sockets, local block files). Chunks of stripes flow
-// through a ring of device slots, one stream each: H2D of exactly the rows
-// the chunk's codes read -> kernel -> D2H of exactly the rows they write.
+// through a ring of device slots: H2D of exactly the rows the chunk's codes
+// read (on the copy-in stream) -> kernel (on the slot's stream) -> D2H of
+// exactly the rows they write (on the copy-out stream), chained by events,
+// so one chunk's D2H overlaps the next chunks' H2D on the full-duplex link.
 // Pinned caller buffers are DMA'd directly and the whole job is queued before
 // the host waits once; pageable ones go through each slot's pinned staging
 // (copy pool), the host then waits for a slot before refilling it.
@@ -211,15 +213,33 @@ size_t hbatch_target_bytes() {
   return v;
 }
 
+// H2D and D2H on their own streams (one per direction, shared by the slots),
+// or on each slot's stream behind and ahead of its kernels (HRS_HBATCH_DUPLEX=0:
+// the round-3 pipeline, kept for A/B runs; read per call so one process can
+// interleave both: tools/bench_hbatch.py).
+bool hbatch_duplex() {
+  const char* e = getenv("HRS_HBATCH_DUPLEX");
+  return !(e && e[0] == '0');
+}
+
 hrs_status hbatch_slot(hrs_codec* c, int i, size_t dev_bytes, size_t pin_bytes) {
   hrs_codec::HostBatchSlot& h = c->hbatch[i];
   if (!h.stream) {
     hipError_t e = hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(c, e, "hipStreamCreate");
-    e = hipEventCreateWithFlags(&h.done, hipEventDisableTiming);
-    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+    for (hipEvent_t* ev : {&h.done, &h.in_done, &h.comp_done}) {
+      e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+      if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+    }
   }
+  for (hipStream_t* s : {&c->hbatch_in, &c->hbatch_out})
+    if (!*s) {
+      hipError_t e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+      if (e != hipSuccess) return hip_fail(c, e, "hipStreamCreate");
+    }
   if (h.dev_bytes < dev_bytes) {
+    (void)hipStreamSynchronize(c->hbatch_in);
+    (void)hipStreamSynchronize(c->hbatch_out);
     (void)hipStreamSynchronize(h.stream);
     if (h.dev) (void)hipFree(h.dev);
     h.dev = nullptr;
@@ -229,6 +249,8 @@ hrs_status hbatch_slot(hrs_codec* c, int i, size_t dev_bytes, size_t pin_bytes) 
     h.dev_bytes = dev_bytes;
   }
   if (h.pin_bytes < pin_bytes) {
+    (void)hipStreamSynchronize(c->hbatch_in);
+    (void)hipStreamSynchronize(c->hbatch_out);
     (void)hipStreamSynchronize(h.stream);
     if (h.pin) (void)hipHostFree(h.pin);
     h.pin = nullptr;
@@ -306,8 +328,10 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
   }
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
+  const bool duplex = hbatch_duplex();
   struct Pending {
     bool busy = false;
+    bool used = false;  // the slot's events have been recorded by this call
     size_t s0 = 0, ns = 0;
   } pend[hrs::kHostBatchSlots];
   // pageable: wait for a slot, then copy its outputs out of staging
@@ -346,26 +370,44 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
           }
       pool.run(jobs);
     }
+    // stream of each stage; in duplex mode the H2D waits until the slot's
+    // previous kernels have read its image, the kernels until the previous
+    // D2H has read its output block, the D2H until this chunk's kernels
+    const hipStream_t s_in = duplex ? c->hbatch_in : h.stream;
+    const hipStream_t s_out = duplex ? c->hbatch_out : h.stream;
+    hipError_t e = hipSuccess;
+    if (duplex && pend[sl].used && (e = hipStreamWaitEvent(s_in, h.comp_done, 0)) != hipSuccess)
+      return hip_fail(c, e, "hipStreamWaitEvent");
     uint8_t* dimg = h.dev;
     uint8_t* dout = h.dev + chunk * img_stripe;
     for (size_t i = 0; i < ns; ++i) {
       const uint8_t* src = pinned ? hin + (s0 + i) * in_stripe : h.pin + i * img_stripe;
       hrs_status st = h2d_runs(c, reads(s0 + i), dimg + i * img_stripe, dpitch, src, pinned ? in_row : dpitch, len,
-                               h.stream);
+                               s_in);
       if (st != HRS_OK) return st;
+    }
+    if (duplex) {
+      if ((e = hipEventRecord(h.in_done, s_in)) != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+      if ((e = hipStreamWaitEvent(h.stream, h.in_done, 0)) != hipSuccess) return hip_fail(c, e, "hipStreamWaitEvent");
+      if (pend[sl].used && (e = hipStreamWaitEvent(h.stream, h.done, 0)) != hipSuccess)
+        return hip_fail(c, e, "hipStreamWaitEvent");
     }
     hrs_status st = compute(h.stream, s0, ns, dimg, img_stripe, dpitch, dout, out_stripe_dev);
     if (st != HRS_OK) return st;
+    if (duplex) {
+      if ((e = hipEventRecord(h.comp_done, h.stream)) != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+      if ((e = hipStreamWaitEvent(s_out, h.comp_done, 0)) != hipSuccess) return hip_fail(c, e, "hipStreamWaitEvent");
+    }
     for (size_t i = 0; i < ns; ++i) {
       const size_t s = s0 + i;
-      st = pinned ? d2h_rows(c, hout + s * out_stripe, out_row, dout + i * out_stripe_dev, dpitch, len, writes(s), h.stream)
+      st = pinned ? d2h_rows(c, hout + s * out_stripe, out_row, dout + i * out_stripe_dev, dpitch, len, writes(s), s_out)
                   : d2h_rows(c, h.pin + chunk * img_stripe + i * out_stripe_dev, dpitch, dout + i * out_stripe_dev,
-                             dpitch, len, writes(s), h.stream);
+                             dpitch, len, writes(s), s_out);
       if (st != HRS_OK) return st;
     }
-    hipError_t e = hipEventRecord(h.done, h.stream);
-    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+    if ((e = hipEventRecord(h.done, s_out)) != hipSuccess) return hip_fail(c, e, "hipEventRecord");
     pend[sl].busy = true;
+    pend[sl].used = true;
     pend[sl].s0 = s0;
     pend[sl].ns = ns;
   }
@@ -378,9 +420,12 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
 
 // A failed host batch may leave slot work in flight: drain every slot stream.
 hrs_status drain_hbatch(hrs_codec* c, hrs_status st) {
-  if (st != HRS_OK)
+  if (st != HRS_OK) {
+    for (hipStream_t s : {c->hbatch_in, c->hbatch_out})
+      if (s) (void)hipStreamSynchronize(s);
     for (auto& h : c->hbatch)
       if (h.stream) (void)hipStreamSynchronize(h.stream);
+  }
   return st;
 }
 

@@ -67,7 +67,10 @@ struct hrs_codec {
   } host[2];
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
-  // its own stream
+  // its own compute stream; every slot's H2D goes on one copy-in stream and
+  // every D2H on one copy-out stream, so the two directions of the link run
+  // at once (the link is full duplex: profiles/r04/duplex/). Per slot:
+  // in_done after its H2D, comp_done after its kernels, done after its D2H.
   struct HostBatchSlot {
     uint8_t* dev = nullptr;
     size_t dev_bytes = 0;
@@ -75,7 +78,11 @@ struct hrs_codec {
     size_t pin_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    hipEvent_t in_done = nullptr;
+    hipEvent_t comp_done = nullptr;
   } hbatch[hrs::kHostBatchSlots];
+  hipStream_t hbatch_in = nullptr;   // H2D of every host-batch slot
+  hipStream_t hbatch_out = nullptr;  // D2H of every host-batch slot
   // asynchronous host-buffer calls (hrs_*_submit / hrs_collect): a ring of
   // operation slots, each pinned staging + device rows + its own stream; an
   // operation occupies its slot from submit until it is collected

@@ -1,5 +1,7 @@
-// HBM ceiling probes (include/hrs_probe.h), built into libhrs so bench.py
-// measures its own ceilings beside the coding kernels in the same run:
+// HBM ceiling probes (include/hrs_probe.h), built as their own library,
+// libhrs_probe.so: bench.py and tools load it to measure this GPU's ceilings
+// beside the coding kernels in the same run; the product library a DataNode
+// JVM loads (libhrs.so) does not carry them.
 //   - streams (copy / read-only / write-only) in the shape of round 1's
 //     bandwidth lab (tools/bw_lab.hip, profiles/r01/lab8_bw_ceilings.txt): a
 //     wave task is `chunk` KiB contiguous, one 16-byte access per lane per
@@ -32,46 +34,72 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
   else *p = v;
 }
 
-// Elements [tail0, n) that do not fill a whole chunk: one 16-byte element per
-// thread of the grid (the chunked loop has covered [0, tail0)).
-__device__ __forceinline__ uint64_t tail_index() {
-  return static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+// Stream ops: 0 copy, 1 read-only (XOR kept alive by a data-dependent store
+// to `sink`, practically never taken), 2 write-only; each over n 16-byte
+// elements under one of three schedules (tools/copy_lab.hip measured them,
+// profiles/r04/copy_lab/):
+//   WAVE_TASKS  a wave task is D contiguous KiB (lane l moves the 16 bytes at
+//               1024 j + 16 l of KiB j), wave tasks grid-striding;
+//   GRID_STRIDE thread i moves elements i + j T (T = every thread of the
+//               grid), D of them in flight before any is used;
+//   BLOCK_RANGE block b owns the b-th of gridDim equal ranges and walks it
+//               block-stride, D elements per thread in flight — each block
+//               streams through one contiguous region (the fastest copy on
+//               this pool: 5.75 TB/s against 5.36 for the grid-stride loop).
+template <int OP, bool NT>
+__device__ __forceinline__ void stream_op(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t i,
+                                          u32x4& acc) {
+  if constexpr (OP == 0) st16<NT>(&dst[i], ld16<NT>(&src[i]));
+  else if constexpr (OP == 1) acc ^= ld16<NT>(&src[i]);
+  else st16<NT>(&dst[i], u32x4{static_cast<uint32_t>(i), 0x5A5A5A5Au, ~static_cast<uint32_t>(i), 0u});
 }
 
-// Stream ops: 0 copy, 1 read-only (XOR kept alive by an impossible store to
-// `sink`), 2 write-only. A task is C KiB = 64 * C elements of 16 bytes.
-template <int OP, int C, bool NT>
-__global__ void __launch_bounds__(256) stream_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                      uint64_t n) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t ntasks = n / (64u * C);
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
-  u32x4 acc = {0u, 0u, 0u, 0u};
-  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nw) {
-    const uint64_t e = t * 64u * C + lane;
-    if constexpr (OP == 2) {
-      const uint32_t v = static_cast<uint32_t>(t);
+// D elements at base + j * step (j < D): all loads issued before any store.
+template <int OP, int D, bool NT>
+__device__ __forceinline__ void stream_group(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t base,
+                                             uint64_t step, u32x4& acc) {
+  if constexpr (OP == 2) {
 #pragma unroll
-      for (int j = 0; j < C; ++j) st16<NT>(&dst[e + 64u * j], u32x4{v, 0x5A5A5A5Au, ~v, static_cast<uint32_t>(j)});
-    } else {
-      u32x4 v[C];
+    for (int j = 0; j < D; ++j) stream_op<2, NT>(src, dst, base + j * step, acc);
+  } else {
+    u32x4 v[D];
 #pragma unroll
-      for (int j = 0; j < C; ++j) v[j] = ld16<NT>(&src[e + 64u * j]);
+    for (int j = 0; j < D; ++j) v[j] = ld16<NT>(&src[base + j * step]);
 #pragma unroll
-      for (int j = 0; j < C; ++j) {
-        if constexpr (OP == 0) st16<NT>(&dst[e + 64u * j], v[j]);
-        else acc ^= v[j];
-      }
+    for (int j = 0; j < D; ++j) {
+      if constexpr (OP == 0) st16<NT>(&dst[base + j * step], v[j]);
+      else acc ^= v[j];
     }
   }
-  const uint64_t i = ntasks * 64u * C + tail_index();
-  if (i < n) {
-    if constexpr (OP == 0) dst[i] = src[i];
-    else if constexpr (OP == 1) acc ^= src[i];
-    else dst[i] = u32x4{0u, 0x5A5A5A5Au, ~0u, 0u};
+}
+
+template <int OP, int SCHED, int D, bool NT>
+__global__ void __launch_bounds__(1024) stream_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       uint64_t n) {
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  const uint64_t T = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if constexpr (SCHED == HRS_PROBE_WAVE_TASKS) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t ntasks = n / (64u * D);
+    const uint64_t nw = T >> 6;
+    for (uint64_t t = gid >> 6; t < ntasks; t += nw) stream_group<OP, D, NT>(src, dst, t * 64u * D + lane, 64u, acc);
+    for (uint64_t i = ntasks * 64u * D + gid; i < n; i += T) stream_op<OP, false>(src, dst, i, acc);
+  } else if constexpr (SCHED == HRS_PROBE_GRID_STRIDE) {
+    uint64_t i = gid;
+    for (; i + (D - 1) * T < n; i += D * T) stream_group<OP, D, NT>(src, dst, i, T, acc);
+    for (; i < n; i += T) stream_op<OP, false>(src, dst, i, acc);
+  } else {
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = per * blockIdx.x;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    const uint64_t B = blockDim.x;
+    uint64_t i = lo + threadIdx.x;
+    for (; i + (D - 1) * B < hi; i += D * B) stream_group<OP, D, NT>(src, dst, i, B, acc);
+    for (; i < hi; i += B) stream_op<OP, false>(src, dst, i, acc);
   }
   if constexpr (OP == 1)
-    if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9E3779B9u && acc[0] == 0x7F4A7C15u) dst[threadIdx.x] = acc;
+    if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9E3779B9u && acc[0] == 0x7F4A7C15u) dst[threadIdx.x & 255] = acc;
 }
 
 // The codec's access pattern without the GF math: task t = (stripe, 2 KiB
@@ -127,26 +155,38 @@ __global__ void __launch_bounds__(256) rows_kernel(uint8_t* __restrict__ base, u
   }
 }
 
-template <int OP, int C>
-hrs_status launch_stream_c(const void* src, void* dst, uint64_t n, bool nt, unsigned grid, hipStream_t st) {
-  const char* names[3] = {"stream_copy_kernel", "stream_read_kernel", "stream_write_kernel"};
-  note_kernel_t(names[OP], C, nt);
-  auto k = nt ? stream_kernel<OP, C, true> : stream_kernel<OP, C, false>;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), n);
+template <int OP, int SCHED, int D>
+hrs_status launch_stream_d(const void* src, void* dst, uint64_t n, bool nt, unsigned grid, unsigned block,
+                           hipStream_t st) {
+  auto k = nt ? stream_kernel<OP, SCHED, D, true> : stream_kernel<OP, SCHED, D, false>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, st, static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), n);
   return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
 }
 
+template <int OP, int SCHED>
+hrs_status launch_stream_s(const void* src, void* dst, uint64_t n, int depth, bool nt, unsigned grid, unsigned block,
+                           hipStream_t st) {
+  switch (depth) {
+    case 1: return launch_stream_d<OP, SCHED, 1>(src, dst, n, nt, grid, block, st);
+    case 2: return launch_stream_d<OP, SCHED, 2>(src, dst, n, nt, grid, block, st);
+    case 4: return launch_stream_d<OP, SCHED, 4>(src, dst, n, nt, grid, block, st);
+    default: return launch_stream_d<OP, SCHED, 8>(src, dst, n, nt, grid, block, st);
+  }
+}
+
 template <int OP>
-hrs_status launch_stream(const void* src, void* dst, size_t bytes, int chunk_kib, int nt, int bpc, void* stream) {
+hrs_status launch_stream(const void* src, void* dst, size_t bytes, int schedule, int depth, int nt, int block,
+                         int bpc, void* stream) {
   const unsigned grid = static_cast<unsigned>(bpc * device_cus());
   const uint64_t n = bytes / 16;
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  switch (chunk_kib) {
-    case 1: return launch_stream_c<OP, 1>(src, dst, n, nt != 0, grid, st);
-    case 2: return launch_stream_c<OP, 2>(src, dst, n, nt != 0, grid, st);
-    case 4: return launch_stream_c<OP, 4>(src, dst, n, nt != 0, grid, st);
-    case 8: return launch_stream_c<OP, 8>(src, dst, n, nt != 0, grid, st);
-    default: return HRS_EINVAL;
+  switch (schedule) {
+    case HRS_PROBE_WAVE_TASKS:
+      return launch_stream_s<OP, HRS_PROBE_WAVE_TASKS>(src, dst, n, depth, nt != 0, grid, block, st);
+    case HRS_PROBE_GRID_STRIDE:
+      return launch_stream_s<OP, HRS_PROBE_GRID_STRIDE>(src, dst, n, depth, nt != 0, grid, block, st);
+    default:
+      return launch_stream_s<OP, HRS_PROBE_BLOCK_RANGE>(src, dst, n, depth, nt != 0, grid, block, st);
   }
 }
 
@@ -154,7 +194,6 @@ hrs_status launch_stream(const void* src, void* dst, size_t bytes, int chunk_kib
 // first, no math; 1 = (3, 12); 2 = (5, 6); 3 = (1, 0).
 template <int R, int W, int D, int M>
 hrs_status launch_rows_dm(void* base, size_t nstripes, int nrows, size_t L, unsigned grid, hipStream_t st) {
-  note_kernel_t("probe_rows_kernel", R, W, D, M);
   auto k = rows_kernel<R, W, D, M>;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<uint8_t*>(base), static_cast<uint64_t>(nstripes),
                      nrows, static_cast<uint64_t>(L));
@@ -172,38 +211,32 @@ hrs_status launch_rows_rw(void* base, size_t nstripes, int nrows, size_t L, int 
   }
 }
 
-bool stream_args_ok(int chunk_kib, int bpc) {
-  return bpc >= 1 && bpc <= 32 && (chunk_kib == 1 || chunk_kib == 2 || chunk_kib == 4 || chunk_kib == 8);
+bool stream_args_ok(int schedule, int depth, int block, int bpc) {
+  return schedule >= HRS_PROBE_WAVE_TASKS && schedule <= HRS_PROBE_BLOCK_RANGE &&
+         (depth == 1 || depth == 2 || depth == 4 || depth == 8) && (block == 256 || block == 512 || block == 1024) &&
+         bpc >= 1 && bpc * block <= 8192;
 }
 
 }  // namespace
 }  // namespace hrs
 
-extern "C" hrs_status hrs_probe_stream(int op, const void* src, void* dst, size_t bytes, int chunk_kib,
-                                       int nontemporal, int blocks_per_cu, void* stream) {
-  if (op < HRS_PROBE_COPY || op > HRS_PROBE_WRITE || !hrs::stream_args_ok(chunk_kib, blocks_per_cu)) return HRS_EINVAL;
+extern "C" hrs_status hrs_probe_stream(int op, const void* src, void* dst, size_t bytes, int schedule, int depth,
+                                       int nontemporal, int block_threads, int blocks_per_cu, void* stream) {
+  if (op < HRS_PROBE_COPY || op > HRS_PROBE_WRITE || !hrs::stream_args_ok(schedule, depth, block_threads, blocks_per_cu))
+    return HRS_EINVAL;
   const bool need_src = op != HRS_PROBE_WRITE;
   if (bytes && ((need_src && !src) || !dst)) return HRS_EINVAL;
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) return HRS_EALIGN;
   if (bytes == 0) return HRS_OK;
   switch (op) {
-    case HRS_PROBE_COPY: return hrs::launch_stream<0>(src, dst, bytes, chunk_kib, nontemporal, blocks_per_cu, stream);
-    case HRS_PROBE_READ: return hrs::launch_stream<1>(src, dst, bytes, chunk_kib, nontemporal, blocks_per_cu, stream);
-    default: return hrs::launch_stream<2>(nullptr, dst, bytes, chunk_kib, nontemporal, blocks_per_cu, stream);
+    case HRS_PROBE_COPY:
+      return hrs::launch_stream<0>(src, dst, bytes, schedule, depth, nontemporal, block_threads, blocks_per_cu, stream);
+    case HRS_PROBE_READ:
+      return hrs::launch_stream<1>(src, dst, bytes, schedule, depth, nontemporal, block_threads, blocks_per_cu, stream);
+    default:
+      return hrs::launch_stream<2>(nullptr, dst, bytes, schedule, depth, nontemporal, block_threads, blocks_per_cu,
+                                   stream);
   }
-}
-
-extern "C" hrs_status hrs_probe_copy(const void* src, void* dst, size_t bytes, int blocks_per_cu, void* stream) {
-  return hrs_probe_stream(HRS_PROBE_COPY, src, dst, bytes, 1, 1, blocks_per_cu, stream);
-}
-
-extern "C" hrs_status hrs_probe_read(const void* src, size_t bytes, int blocks_per_cu, void* sink, void* stream) {
-  if (!sink) return HRS_EINVAL;
-  return hrs_probe_stream(HRS_PROBE_READ, src, sink, bytes, 1, 1, blocks_per_cu, stream);
-}
-
-extern "C" hrs_status hrs_probe_write(void* dst, size_t bytes, int blocks_per_cu, void* stream) {
-  return hrs_probe_stream(HRS_PROBE_WRITE, nullptr, dst, bytes, 1, 1, blocks_per_cu, stream);
 }
 
 extern "C" hrs_status hrs_probe_rows(void* base, size_t nstripes, int nrows, size_t cell_bytes, int nread,

@@ -223,41 +223,54 @@ def crc32_rows(code, row_views, crc_in=None):
 
 
 PROBE_COPY, PROBE_READ, PROBE_WRITE = 0, 1, 2
+WAVE_TASKS, GRID_STRIDE, BLOCK_RANGE = 0, 1, 2  # hrs_probe_stream schedules
 
 
 def _nbytes(t):
     return t.numel() * t.element_size()
 
 
-def probe_copy(src, dst, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
-    """HBM ceiling probe (include/hrs_probe.h, hrs_probe_stream): dst <- src,
-    both contiguous device tensors of the same byte size; wave tasks of
-    `chunk_kib` contiguous KiB at `blocks_per_cu` 256-thread blocks per CU,
-    on the current stream. Diagnostic: bench.py's copy_peak."""
+def _probe_check(status):
+    if status != _lib.HRS_OK:
+        raise _lib.HrsError(status, "hrs_probe call rejected its arguments")
+
+
+def _probe_stream(op, src, dst, schedule, depth, nontemporal, block_threads, blocks_per_cu, nbytes, stream):
+    _probe_check(_lib.probe_lib().hrs_probe_stream(op, src, dst, nbytes, int(schedule), int(depth),
+                                                   int(bool(nontemporal)), int(block_threads), int(blocks_per_cu),
+                                                   stream))
+
+
+def probe_copy(src, dst, schedule=BLOCK_RANGE, depth=8, nontemporal=True, block_threads=1024, blocks_per_cu=1):
+    """HBM ceiling probe (libhrs_probe.so, hrs_probe_stream COPY): dst <- src,
+    both contiguous device tensors of the same byte size, on the current
+    stream. Diagnostic: bench.py's copy_peak. Default = the fastest copy
+    schedule of tools/copy_lab.hip (block ranges, 8 in flight, nontemporal,
+    one 1024-thread block per CU)."""
     if (not src.is_cuda or not dst.is_cuda or not src.is_contiguous() or not dst.is_contiguous()
             or _nbytes(dst) != _nbytes(src)):
         raise ValueError("probe_copy needs two contiguous device tensors of equal size")
-    _lib.check(_lib.lib().hrs_probe_stream(PROBE_COPY, src.data_ptr(), dst.data_ptr(), _nbytes(src), int(chunk_kib),
-                                           int(bool(nontemporal)), int(blocks_per_cu), _stream(src)))
+    _probe_stream(PROBE_COPY, src.data_ptr(), dst.data_ptr(), schedule, depth, nontemporal, block_threads,
+                  blocks_per_cu, _nbytes(src), _stream(src))
 
 
-def probe_read(src, sink, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
+def probe_read(src, sink, schedule=BLOCK_RANGE, depth=8, nontemporal=True, block_threads=1024, blocks_per_cu=1):
     """HBM read-only probe (hrs_probe_stream READ): reads the contiguous
     device tensor `src` once; `sink` is a device tensor of >= 4 KiB (never
     written in practice)."""
     if not src.is_cuda or not src.is_contiguous() or not sink.is_cuda or _nbytes(sink) < 4096:
         raise ValueError("probe_read needs a contiguous device tensor and a 4 KiB device sink")
-    _lib.check(_lib.lib().hrs_probe_stream(PROBE_READ, src.data_ptr(), sink.data_ptr(), _nbytes(src), int(chunk_kib),
-                                           int(bool(nontemporal)), int(blocks_per_cu), _stream(src)))
+    _probe_stream(PROBE_READ, src.data_ptr(), sink.data_ptr(), schedule, depth, nontemporal, block_threads,
+                  blocks_per_cu, _nbytes(src), _stream(src))
 
 
-def probe_write(dst, blocks_per_cu=4, chunk_kib=1, nontemporal=True):
+def probe_write(dst, schedule=BLOCK_RANGE, depth=8, nontemporal=True, block_threads=1024, blocks_per_cu=1):
     """HBM write-only probe (hrs_probe_stream WRITE): writes the contiguous
     device tensor `dst` once."""
     if not dst.is_cuda or not dst.is_contiguous():
         raise ValueError("probe_write needs a contiguous device tensor")
-    _lib.check(_lib.lib().hrs_probe_stream(PROBE_WRITE, None, dst.data_ptr(), _nbytes(dst), int(chunk_kib),
-                                           int(bool(nontemporal)), int(blocks_per_cu), _stream(dst)))
+    _probe_stream(PROBE_WRITE, None, dst.data_ptr(), schedule, depth, nontemporal, block_threads, blocks_per_cu,
+                  _nbytes(dst), _stream(dst))
 
 
 def probe_rows(stripes, nread, nwrite, blocks_per_cu=2, schedule=0):
@@ -270,5 +283,5 @@ def probe_rows(stripes, nread, nwrite, blocks_per_cu=2, schedule=0):
             or not stripes.is_contiguous()):
         raise ValueError("probe_rows needs a contiguous uint8 device tensor [S, nrows, L]")
     S, n, L = stripes.shape
-    _lib.check(_lib.lib().hrs_probe_rows(stripes.data_ptr(), S, n, L, int(nread), int(nwrite), int(schedule),
-                                         int(blocks_per_cu), _stream(stripes)))
+    _probe_check(_lib.probe_lib().hrs_probe_rows(stripes.data_ptr(), S, n, L, int(nread), int(nwrite),
+                                                 int(schedule), int(blocks_per_cu), _stream(stripes)))

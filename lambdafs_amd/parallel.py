@@ -5,7 +5,9 @@ rank encodes/decodes its own contiguous stripe range. torch.distributed
 (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in CPU tests) carries only
   - the coding matrix, broadcast from rank 0 and checked by every rank
     against the one it built itself (a cheap cross-rank consistency check), and
-  - the barriers and the max-over-ranks reduction around timed regions.
+  - the barriers and the max-over-ranks reduction around timed regions, and
+  - after timing, small gathers of per-rank evidence (output digests, kernel
+    times) for rank 0's report.
 """
 import numpy as np
 import torch
@@ -59,6 +61,24 @@ def max_over_ranks(x, device="cpu"):
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def min_over_ranks(x, device="cpu"):
+    """Smallest int over the ranks (every rank gets it)."""
+    if not active():
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def gather_objects(obj):
+    """[obj of rank 0, obj of rank 1, ...] on every rank (all_gather_object)."""
+    if not active():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def all_ok(flag, device="cpu"):

@@ -586,6 +586,231 @@ int orc_apache_rs_decode(int k, int p, uint8_t* const* inputs, const int* erased
   return rc;
 }
 
+/* ------------------------------------- hadoop-common's legacy RS coder
+ * The reference's second source of the SAME polynomial code as hops'
+ * ReedSolomonCode: hadoop-common
+ * .../io/erasurecode/rawcoder/RSLegacyRawEncoder.java, RSLegacyRawDecoder.java
+ * over its own util/GaloisField.java and util/RSUtil.java — separate files,
+ * restated here loop for loop with their own tables (lg_*), so a slip in one
+ * transcription of the hops classes cannot hide in both. */
+
+/* rawcoder/util/GaloisField.java: int tables of the byte field (field size
+ * 256, primitive polynomial 285: getInstance(), :119-121), built by the
+ * constructor :47-93. */
+static int lg_log[FIELD], lg_pow[FIELD], lg_mul[FIELD][FIELD], lg_div[FIELD][FIELD];
+
+__attribute__((constructor)) static void lg_init(void) {
+  int value = 1;
+  for (int pow = 0; pow < FIELD - 1; pow++) { /* :58-66 */
+    lg_pow[pow] = value;
+    lg_log[value] = pow;
+    value = value * 2;
+    if (value >= FIELD) value = value ^ PRIM_POLY;
+  }
+  for (int i = 0; i < FIELD; i++) /* :68-79 */
+    for (int j = 0; j < FIELD; j++) {
+      if (i == 0 || j == 0) {
+        lg_mul[i][j] = 0;
+        continue;
+      }
+      int z = lg_log[i] + lg_log[j];
+      z = z >= PERIOD ? z - PERIOD : z;
+      lg_mul[i][j] = lg_pow[z];
+    }
+  for (int i = 0; i < FIELD; i++) /* :81-92 (divTable[*][0] stays 0) */
+    for (int j = 1; j < FIELD; j++) {
+      if (i == 0) {
+        lg_div[i][j] = 0;
+        continue;
+      }
+      int z = lg_log[i] - lg_log[j];
+      z = z < 0 ? z + PERIOD : z;
+      lg_div[i][j] = lg_pow[z];
+    }
+}
+
+/* GaloisField.power, :184-198 */
+static int lg_power(int x, int n) {
+  if (n == 0) return 1;
+  if (x == 0) return 0;
+  x = lg_log[x] * n;
+  if (x < PERIOD) return lg_pow[x];
+  x = x % PERIOD;
+  return lg_pow[x];
+}
+
+/* RSUtil.getPrimitivePower, RSUtil.java:38-45: primitivePower[i] = 2^i. */
+static void lg_primitive_power(int k, int p, int* pp) {
+  for (int i = 0; i < k + p; i++) pp[i] = lg_power(2, i);
+}
+
+/* RSLegacyRawEncoder(ErasureCoderOptions), RSLegacyRawEncoder.java:36-53:
+ * gen = prod_{i<p} (x + primitivePower[i]) through GaloisField.multiply(int[],
+ * int[]) (:315-328, add = xor :148-151). Returns p + 1 coefficients. */
+static void lg_generator(int k, int p, int* gen) {
+  int pp[256], tmp[257];
+  lg_primitive_power(k, p, pp);
+  int glen = 1;
+  gen[0] = 1;
+  for (int i = 0; i < p; i++) {
+    const int poly[2] = {pp[i], 1};
+    for (int t = 0; t < glen + 1; t++) tmp[t] = 0;
+    for (int a = 0; a < glen; a++)
+      for (int b = 0; b < 2; b++) tmp[a + b] = tmp[a + b] ^ lg_mul[gen[a]][poly[b]];
+    glen += 1;
+    for (int t = 0; t < glen; t++) gen[t] = tmp[t];
+  }
+}
+
+int orc_legacy_generator(int k, int p, int* gen_out) {
+  if (k + p >= FIELD) return -1; /* the constructor's assert, :39 */
+  lg_generator(k, p, gen_out);
+  return p + 1;
+}
+
+/* RSLegacyRawEncoder.doEncode(ByteArrayEncodingState), :91-128, with
+ * allowChangeInputs() false (the coder's default): outputs zeroed
+ * (CoderUtil.resetOutputBuffers), inputs copied (Arrays.copyOfRange), all =
+ * [outputs..., input copies...], then GaloisField.remainder(byte[][], int[]
+ * offsets, int len, int[] divisor), util/GaloisField.java:480-495 (every
+ * offset 0 here). inputs: the k data units, outputs: the p parity units. */
+void orc_legacy_rs_encode(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len) {
+  int gen[257];
+  lg_generator(k, p, gen);
+  const int nv = p + 1, nd = k + p;
+  uint8_t** all = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)nd);
+  for (int i = 0; i < p; i++) {
+    memset(outputs[i], 0, len);
+    all[i] = outputs[i];
+  }
+  for (int i = 0; i < k; i++) {
+    all[p + i] = (uint8_t*)malloc(len ? len : 1);
+    memcpy(all[p + i], inputs[i], len);
+  }
+  for (int i = nd - nv; i >= 0; i--)
+    for (int j = 0; j < nv; j++)
+      for (size_t idx = 0; idx < len; idx++) {
+        const int ratio = lg_div[all[i + nv - 1][idx] & 0xFF][gen[nv - 1]];
+        all[j + i][idx] = (uint8_t)((all[j + i][idx] & 0xFF) ^ lg_mul[ratio][gen[j]]);
+      }
+  for (int i = 0; i < k; i++) free(all[p + i]);
+  free(all);
+}
+
+/* GaloisField.substitute(byte[][] p, int[] offsets, int len, byte[] q, int
+ * offset, int x), util/GaloisField.java:422-434: a null unit counts as 0. */
+static void lg_substitute(uint8_t* const* pu, int np, size_t len, uint8_t* q, int x) {
+  int y = 1;
+  for (int i = 0; i < np; i++) {
+    const uint8_t* pi = pu[i];
+    for (size_t idx = 0; idx < len; idx++) {
+      const int pij = pi != NULL ? pi[idx] & 0xFF : 0;
+      q[idx] = (uint8_t)(q[idx] ^ lg_mul[pij][y]);
+    }
+    y = lg_mul[x][y];
+  }
+}
+
+/* GaloisField.solveVandermondeSystem(int[] x, byte[][] y, int[] outputOffsets,
+ * int len, int dataLen), util/GaloisField.java:241-268. */
+static void lg_solve_vandermonde(const int* x, uint8_t* const* y, int len, size_t data_len) {
+  for (int i = 0; i < len - 1; i++)
+    for (int j = len - 1; j > i; j--)
+      for (size_t idx = 0; idx < data_len; idx++) y[j][idx] = (uint8_t)(y[j][idx] ^ lg_mul[x[i]][y[j - 1][idx] & 0xFF]);
+  for (int i = len - 1; i >= 0; i--) {
+    for (int j = i + 1; j < len; j++)
+      for (size_t idx = 0; idx < data_len; idx++) y[j][idx] = (uint8_t)lg_div[y[j][idx] & 0xFF][x[j] ^ x[j - i - 1]];
+    for (int j = i; j < len - 1; j++)
+      for (size_t idx = 0; idx < data_len; idx++) y[j][idx] = (uint8_t)(y[j][idx] ^ y[j + 1][idx]);
+  }
+}
+
+/* RSLegacyRawDecoder.decode(byte[][] inputs, int[] erasedIndexes, byte[][]
+ * outputs), RSLegacyRawDecoder.java:71-83, in the caller's order: inputs =
+ * the n units [data 0..k-1, parity 0..p-1], NULL for a unit not read (erased
+ * or not to read); outputs[t] receives unit erased[t].
+ *   adjustOrder, :222-253: units to [parity..., data...]; erased parity
+ *     indexes first (- k), then erased data (+ p); outputs reordered alike;
+ *   ByteArrayDecodingState, ByteArrayDecodingState.java:37-52, 95-115:
+ *     at least k non-null inputs (else HadoopIllegalArgumentException: -1);
+ *   doDecode(ByteArrayDecodingState), :111-165: outputs zeroed; every null
+ *     unit (CoderUtil.getNullIndexes, CoderUtil.java:146-156) gets an output
+ *     slot — the caller's buffer where it is an erased index (else -2: the
+ *     "not fully corresponding" exception), a scratch buffer otherwise; more
+ *     null units than p overflow the p-slot arrays (-3: Java's
+ *     ArrayIndexOutOfBoundsException);
+ *   doDecodeImpl, :98-109: errSignature[i] = primitivePower[null_i], slot i
+ *     = substitute(units, primitivePower[i]) for i < #nulls, then the
+ *     Vandermonde solve over the #nulls slots. */
+int orc_legacy_rs_decode(int k, int p, uint8_t* const* inputs, const int* erased, int ne, uint8_t* const* outputs,
+                         size_t len) {
+  const int n = k + p;
+  uint8_t* units[256];
+  int erased2[256];
+  uint8_t* outputs2[256];
+  for (int i = 0; i < p; i++) units[i] = inputs[k + i]; /* adjustOrder :227-230 */
+  for (int i = 0; i < k; i++) units[p + i] = inputs[i];
+  int idx = 0, ned = 0, nep = 0;
+  for (int i = 0; i < ne; i++)
+    if (erased[i] >= k) {
+      erased2[idx++] = erased[i] - k;
+      nep++;
+    }
+  for (int i = 0; i < ne; i++)
+    if (erased[i] < k) {
+      erased2[idx++] = erased[i] + p;
+      ned++;
+    }
+  for (int i = 0; i < nep; i++) outputs2[i] = outputs[ned + i]; /* :248-252 */
+  for (int i = 0; i < ned; i++) outputs2[nep + i] = outputs[i];
+  if (len == 0) return 0; /* RawErasureDecoder.decode :138-140 */
+  int valid = 0;
+  for (int i = 0; i < n; i++) valid += units[i] != NULL;
+  if (valid < k) return -1;
+  for (int t = 0; t < ne; t++) memset(outputs2[t], 0, len);
+  int nulls[256], nn = 0;
+  for (int i = 0; i < n; i++)
+    if (units[i] == NULL) nulls[nn++] = i;
+  uint8_t* adjusted[256] = {0};
+  uint8_t* scratch[256] = {0};
+  int rc = 0;
+  for (int out_idx = 0, i = 0; i < ne && rc == 0; i++) {
+    int found = 0;
+    for (int j = 0; j < nn; j++)
+      if (erased2[i] == nulls[j]) {
+        found = 1;
+        if (j >= p) {
+          rc = -3;
+          break;
+        }
+        memset(outputs2[out_idx], 0, len);
+        adjusted[j] = outputs2[out_idx];
+        out_idx++;
+      }
+    if (!found && rc == 0) rc = -2;
+  }
+  for (int buf = 0, i = 0; i < nn && rc == 0; i++)
+    if (adjusted[i] == NULL) {
+      if (i >= p || buf >= p) {
+        rc = -3;
+        break;
+      }
+      scratch[buf] = (uint8_t*)calloc(len, 1);
+      adjusted[i] = scratch[buf++];
+    }
+  if (rc == 0) {
+    int pp[256], sig[256];
+    lg_primitive_power(k, p, pp);
+    for (int i = 0; i < nn; i++) {
+      sig[i] = pp[nulls[i]];
+      lg_substitute(units, n, len, adjusted[i], pp[i]);
+    }
+    lg_solve_vandermonde(sig, adjusted, nn, len);
+  }
+  for (int i = 0; i < p; i++) free(scratch[i]);
+  return rc;
+}
+
 /* ------------------------------------------------- nrs (ISA-L Cauchy RS) */
 
 /* ISA-L gf_mul / gf_inv over 0x11D: the same field as GaloisField (285). */

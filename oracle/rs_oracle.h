@@ -123,6 +123,17 @@ void orc_src_encode_bulk(int k, int p, int s_in, uint8_t* const* inputs, uint8_t
 int orc_src_decode_bulk(int k, int p, int s_in, uint8_t* const* read_bufs, uint8_t* const* write_bufs,
                         const int* erased, int ne, const int* to_read, int nr, const int* ntr, int nn, size_t len);
 
+/* hadoop-common's legacy pure-Java RS coder (io/erasurecode/rawcoder/
+ * RSLegacyRawEncoder.java, RSLegacyRawDecoder.java, util/GaloisField.java,
+ * util/RSUtil.java): the same polynomial code as hops' ReedSolomonCode, in
+ * the Apache unit order [data..., parity...]. Decode: inputs NULL for units
+ * not read; outputs[t] = unit erased[t]; 0, or -1 (fewer than k inputs), -2
+ * (an erased unit is not NULL), -3 (more NULL units than p). */
+int orc_legacy_generator(int k, int p, int* gen_out);
+void orc_legacy_rs_encode(int k, int p, uint8_t* const* inputs, uint8_t* const* outputs, size_t len);
+int orc_legacy_rs_decode(int k, int p, uint8_t* const* inputs, const int* erased, int ne, uint8_t* const* outputs,
+                         size_t len);
+
 #ifdef __cplusplus
 }
 #endif

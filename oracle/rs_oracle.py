@@ -73,6 +73,9 @@ def lib():
             "orc_apache_gen_cauchy": ([ctypes.c_void_p, I, I], None),
             "orc_apache_rs_encode": ([I, I, PP, PP, S], None),
             "orc_apache_rs_decode": ([I, I, PP, IP, I, PP, S], I),
+            "orc_legacy_generator": ([I, I, IP], I),
+            "orc_legacy_rs_encode": ([I, I, PP, PP, S], None),
+            "orc_legacy_rs_decode": ([I, I, PP, IP, I, PP, S], I),
             "orc_src_params": ([I, I, I, IP, IP, IP], I),
             "orc_src_encode": ([I, I, I, IP, IP], None),
             "orc_src_decode5": ([I, I, I, IP, IP, I, IP, IP, I, IP, I], I),
@@ -328,6 +331,60 @@ def hops_nrs_decode_via_apache(k, p, read_bufs, erased, not_to_read):
     mod.sort()
     outs = apache_rs_decode(k, p, units, mod)
     return outs[:len(erased)]
+
+
+# ------------- hadoop-common's legacy RS coder (RSLegacyRawEncoder / Decoder)
+
+def legacy_generator(k, p):
+    g = (ctypes.c_int * (p + 1))()
+    assert lib().orc_legacy_generator(k, p, g) == p + 1
+    return list(g)
+
+
+def legacy_rs_encode(k, p, inputs):
+    """RSLegacyRawEncoder.encode: k data units -> p parity units (the same
+    polynomial code as ReedSolomonCode.encodeBulk)."""
+    rows = [np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    outs = [np.zeros(rows[0].size, dtype=np.uint8) for _ in range(p)]
+    lib().orc_legacy_rs_encode(k, p, _rowptrs(rows), _rowptrs(outs), rows[0].size)
+    return outs
+
+
+def legacy_rs_decode(k, p, inputs, erased):
+    """RSLegacyRawDecoder.decode: inputs[k + p] in Apache order [data,
+    parity] (None = not read), erased Apache indexes -> their values, in the
+    order given. Raises ValueError where the Java throws."""
+    rows = [None if r is None else np.ascontiguousarray(r, dtype=np.uint8) for r in inputs]
+    L = max(r.size for r in rows if r is not None)
+    outs = [np.zeros(L, dtype=np.uint8) for _ in erased]
+    st = lib().orc_legacy_rs_decode(k, p, _rowptrs(rows), _ints(erased), len(erased), _rowptrs(outs), L)
+    if st != 0:
+        raise ValueError({-1: "not enough valid inputs", -2: "inputs not fully corresponding to erasedIndexes",
+                          -3: "more null inputs than parity units"}[st])
+    return outs
+
+
+def hops_to_apache(k, p, loc):
+    """hops location (parity first) -> Apache unit index (data first)."""
+    return loc + k if loc < p else loc - p
+
+
+def hops_decode_via_legacy(k, p, read_bufs, erased, not_to_read):
+    """ReedSolomonCode.decodeBulk 5-arg (ReedSolomonCode.java:191-211) worked
+    by the legacy Apache coder: hops rows [parity, data] -> Apache units, the
+    not-to-read units nulled, the erased units decoded (erased must be a
+    subset of not_to_read, as Decoder.java:303-338 builds them); returns the
+    erased values in hops `erased` order."""
+    n = k + p
+    units = [None] * n
+    ntr = set(not_to_read)
+    for loc in range(n):
+        if loc not in ntr:
+            units[hops_to_apache(k, p, loc)] = read_bufs[loc]
+    ap = sorted(hops_to_apache(k, p, e) for e in erased)
+    outs = legacy_rs_decode(k, p, units, ap)
+    by_unit = dict(zip(ap, outs))
+    return [by_unit[hops_to_apache(k, p, e)] for e in erased]
 
 
 # ------------------------------------------- SimpleRegeneratingCode (src)

@@ -17,13 +17,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NONE = -2  # HRS_DEVICE_NONE
 
 
-def declared_symbols():
-    names = set()
-    for h in ("hrs.h", "hrs_probe.h"):
-        src = open(os.path.join(ROOT, "include", h)).read()
-        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        names |= set(re.findall(r"\b(hrs_[a-z0-9_]+)\s*\(", src))
-    return sorted(names)
+def declared_symbols(header="hrs.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hrs_[a-z0-9_]+)\s*\(", src)))
+
+
+def dynamic_symbols(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True)
+    return {ln.split()[-1] for ln in out.stdout.splitlines() if ln.strip()} 
 
 
 def test_library_exports_every_declared_symbol():
@@ -36,15 +39,20 @@ def test_library_exports_every_declared_symbol():
     assert b"gfx950" in _lib.lib().hrs_version()
 
 
-def test_library_exports_only_the_c_abi():
-    """The version script (lambdafs_amd/csrc/libhrs.map) keeps the C++
-    internals local: the dynamic symbol table holds the declared hrs_*
-    entry points (plus HIP's per-TU __hip_cuid_ markers) and nothing else."""
-    import subprocess
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
-    syms = {ln.split()[-1] for ln in out.stdout.splitlines() if ln.strip()}
-    extra = {s for s in syms if not s.startswith("__hip_cuid_")} - set(declared_symbols())
-    assert not extra, sorted(extra)[:10]
+@pytest.mark.parametrize("path,header", [(_lib.LIB_PATH, "hrs.h"), (_lib.PROBE_LIB_PATH, "hrs_probe.h")])
+def test_library_exports_only_its_header(path, header):
+    """The version scripts (lambdafs_amd/csrc/libhrs.map, libhrs_probe.map)
+    keep the C++ internals local: each library's dynamic symbol table holds
+    exactly the hrs_* entry points its header declares (plus HIP's per-TU
+    __hip_cuid_ markers). In particular the product library carries no
+    diagnostics: the HBM probes live in libhrs_probe.so only."""
+    syms = {s for s in dynamic_symbols(path) if not s.startswith("__hip_cuid_")}
+    assert syms == set(declared_symbols(header)), sorted(syms ^ set(declared_symbols(header)))[:10]
+    if header == "hrs.h":
+        assert not any(s.startswith("hrs_probe") for s in syms)
+        assert b"rows_kernel" not in open(path, "rb").read()  # no probe kernels in the product code object
+    else:
+        assert set(syms) == set(_lib.PROBE_EXPORTS)
 
 
 def test_library_is_gfx950_code_object():

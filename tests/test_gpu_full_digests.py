@@ -1,6 +1,7 @@
 """Full-size parity against the oracle (-m gpu): every
 stripe of the BASELINE workloads, not a sample. The product's outputs on the
-SURVEY §8(d) synthetic stripes are hashed per block of 256 global stripes and
+SURVEY §8(d) synthetic stripes are hashed stripe by stripe, the digests
+combined per block of 256 global stripes (tools/stripe_digests.py), and
 compared with the digests the C oracle computed for the same stripes
 (tests/golden/bench_digests.json, made by tests/golden/make_bench_digests.py
 from oracle/rs_oracle.c — ReedSolomonCode.encodeBulk / decodeBulk 5-arg
@@ -36,8 +37,8 @@ def golden():
 
 
 def digests(rows_of, S, g0=0):
-    import bench
-    return bench.block_sha256(rows_of, S, g0)
+    import stripe_digests as SD
+    return SD.combine(SD.stripe_digests(rows_of, S, g0))
 
 
 def check(got, want):

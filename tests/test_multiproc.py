@@ -85,63 +85,91 @@ def test_stripe_range_partition():
             assert max(h - lo for lo, h in spans) - min(h - lo for lo, h in spans) <= 1
 
 
-def _bench_flow_worker(r, nranks, port, outdir):
-    """bench.py's collective sequence under gloo with host-only handles:
-    matrix broadcasts, the barriers and max-over-ranks around the timed
-    region, the all-ok checks, the per-block digest gathers (parity, decode,
-    config-5 repairs) and their comparison with the oracle's digests, the
-    e2e leg's reductions, and the final barrier — in bench.py's order."""
+def _toy_rows(total, width=64):
+    """Stand-in outputs for `total` global stripes (stripe g: its own bytes)."""
+    g = np.arange(total, dtype=np.uint64)[:, None]
+    return ((g * 2654435761 + np.arange(width, dtype=np.uint64)[None, :] * 40503) >> 7).astype(np.uint8)
+
+
+def _bench_flow_worker(r, nranks, port, outdir, strong):
+    """bench.py's collective sequence under gloo with host-only handles and
+    bench.py's own helpers: the e2e guard's MIN, matrix broadcasts, the
+    barriers and max-over-ranks around the timed region, the per-rank
+    evidence gather, the all-ok checks, the per-stripe digest gathers
+    (parity, decode, config-5 repairs) combined per block and compared with
+    an oracle table, and the final barrier — in bench.py's order. With
+    `strong`, 1,024 stripes are split over the ranks (8 x 128: every 256-block
+    spans two ranks), as `bench.py --strong --stripes 1024 --gpus 8` does."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(nranks))
     import sys
     import torch.distributed as dist
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tools"))
     import bench
+    import stripe_digests as SD
     from lambdafs_amd import HipReedSolomonCode, parallel
+    bench.parallel, bench.SD = parallel, SD
     dist.init_process_group("gloo", rank=r, world_size=nranks)
     try:
         k, p = 10, 4
         code = HipReedSolomonCode(k, p, device=-2)
+        e2e_S = parallel.min_over_ranks(bench.e2e_plan(None if r else 64 << 30, 8)[0])
         erased = [p]
         to_read = sorted(code.locationsToReadForDecode(erased))
         ntr = [x for x in range(k + p) if x not in to_read]
         G = parallel.broadcast_matrix(code.encodeMatrix())
         D = parallel.broadcast_matrix(code.decodeMatrix(erased, ntr))
+        total = 1024 if strong else 1024 * nranks
+        lo, hi = parallel.stripe_range(total, nranks, r) if strong else (r * 1024, (r + 1) * 1024)
         parallel.barrier()
         parallel.barrier()
         elapsed = parallel.max_over_ranks(1.0 + r / 10)
+        per_rank = parallel.gather_objects({"rank": r, "g0": lo, "stripes": hi - lo, "wall_s": 1.0 + r / 10})
         ok = parallel.all_ok(True) and parallel.all_ok(True)
-        golden = bench.load_golden()
-        S, g0 = 1024, r * 1024
-        # each rank's digests: the oracle's own blocks for its global range
-        par = {key: v for key, v in golden["config3"]["parity"].items() if g0 <= int(key) < g0 + S}
-        dec = {key: v for key, v in golden["config3"]["decode"].items() if g0 <= int(key) < g0 + S}
-        digs = {"parity": bench.gather_blocks(par, nranks), "decode": bench.gather_blocks(dec, nranks)}
-        vs = bench.compare_blocks(digs, golden["config3"], ("parity", "decode"))
-        # e2e leg (config 5, 512 stripes per rank)
+        rows = _toy_rows(total)
+        table = {"parity": SD.combine(SD.stripe_digests(lambda a, b: rows[a:b], total, 0)),
+                 "decode": SD.combine(SD.stripe_digests(lambda a, b: rows[a:b] ^ 0x5A, total, 0))}
+        digs = {"parity": bench.oracle_blocks(lambda a, b: rows[lo + a:lo + b], hi - lo, lo),
+                "decode": bench.oracle_blocks(lambda a, b: rows[lo + a:lo + b] ^ 0x5A, hi - lo, lo)}
+        vs = SD.compare(digs, table, ("parity", "decode"), total)
+        # e2e leg (config 5: e2e_S stripes per rank)
         t = [parallel.max_over_ranks(float(r + i)) for i in range(3)]
         ok_e2e = parallel.all_ok(r != nranks + 1)
-        rep = {key: v for key, v in golden["config5"]["repaired"].items() if r * 512 <= int(key) < (r + 1) * 512}
-        rep_all = bench.gather_blocks(rep, nranks)
-        vs5 = bench.compare_blocks({"repaired": rep_all}, golden["config5"], ("repaired",))
+        rep_rows = _toy_rows(e2e_S * nranks, 32)
+        rep = SD.combine(bench.gather_digests(SD.stripe_digests(lambda a, b: rep_rows[r * e2e_S + a:r * e2e_S + b],
+                                                                e2e_S, r * e2e_S)))
+        vs5 = SD.compare({"repaired": rep}, {"repaired": SD.combine(SD.stripe_digests(
+            lambda a, b: rep_rows[a:b], e2e_S * nranks, 0))}, ("repaired",), e2e_S * nranks)
         dist.barrier()
         np.savez(os.path.join(outdir, f"flow{r}.npz"), G=G, D=D, elapsed=elapsed, ok=ok and ok_e2e,
-                 nblocks=vs["blocks"], nrep=vs5["blocks"], t=np.array(t), keys=np.array(sorted(digs["parity"])))
+                 nblocks=vs["blocks"], checked=vs["checked_stripes"], nrep=vs5["blocks"], t=np.array(t),
+                 keys=np.array(sorted(digs["parity"])), ranks=np.array([d["rank"] for d in per_rank]),
+                 e2e_S=e2e_S)
     finally:
         dist.destroy_process_group()
 
 
-def test_bench_collective_flow_world8(tmp_path):
-    """bench.py's multi-rank control flow with 8 ranks
-    (gloo on CPU): no collective is rank-conditional, the per-block digests of
-    8 x 1,024 stripes gather into the full set and match the oracle's, and
+@pytest.mark.parametrize("strong", [False, True])
+def test_bench_collective_flow_world8(tmp_path, strong):
+    """bench.py's multi-rank control flow with
+    8 ranks (gloo on CPU): no collective is rank-conditional, the per-stripe
+    digests of every rank combine into the same blocks as one process would
+    hash — also when strong scaling leaves each rank half a block — and every
+    block is checked; the e2e guard's decision is the same on every rank; and
     every rank returns."""
     port = _free_port()
-    mp.start_processes(_bench_flow_worker, args=(8, port, str(tmp_path)), nprocs=8, join=True, start_method="spawn")
+    mp.start_processes(_bench_flow_worker, args=(8, port, str(tmp_path), strong), nprocs=8, join=True,
+                       start_method="spawn")
     res = [np.load(tmp_path / f"flow{r}.npz") for r in range(8)]
+    nblk = 4 if strong else 32
     for z in res:
         assert float(z["elapsed"]) == 1.7 and bool(z["ok"])
-        assert int(z["nblocks"]) == 64 and int(z["nrep"]) == 16  # 32 parity + 32 decode blocks; 16 repaired
+        assert int(z["nblocks"]) == 2 * nblk and int(z["checked"]) == (1024 if strong else 8192)
+        # rank 0 sees 64 GiB for 8 ranks: the guard shrinks the leg to 256
+        # stripes per rank (one oracle block each), and every rank agrees
+        assert int(z["e2e_S"]) == 256 and int(z["nrep"]) == 8
         assert z["t"].tolist() == [7.0, 8.0, 9.0]
-        assert len(z["keys"]) == 32
+        assert len(z["keys"]) == nblk and all("+" not in k for k in z["keys"].tolist())
+        assert z["ranks"].tolist() == list(range(8))
         assert (z["G"] == res[0]["G"]).all() and (z["D"] == res[0]["D"]).all()

@@ -11,24 +11,28 @@ from lambdafs_amd import _lib, device
 
 
 def test_stream_argument_checks():
-    L = _lib.lib()
+    L = _lib.probe_lib()
     buf = ctypes.create_string_buffer(4096)
     p = ctypes.addressof(buf)
     p16 = (p + 15) & ~15
     ok = 0
-    for op, chunk, bpc in ((3, 1, 1), (-1, 1, 1), (0, 3, 1), (0, 16, 1), (0, 1, 0), (0, 1, 33)):
-        assert L.hrs_probe_stream(op, p16, p16, 1024, chunk, 1, bpc, None) != ok, (op, chunk, bpc)
-    assert L.hrs_probe_stream(0, None, p16, 1024, 1, 1, 1, None) != ok  # copy without a source
-    assert L.hrs_probe_stream(2, None, None, 1024, 1, 1, 1, None) != ok  # write without a destination
-    einval = L.hrs_probe_stream(0, p16, p16, 1024, 3, 1, 1, None)
-    ealign = L.hrs_probe_stream(0, p16 + 1, p16, 1024, 1, 1, 1, None)
+    # (op, schedule, depth, block threads, blocks per CU)
+    for args in ((3, 0, 1, 256, 1), (-1, 0, 1, 256, 1), (0, 3, 1, 256, 1), (0, -1, 1, 256, 1), (0, 0, 3, 256, 1),
+                 (0, 0, 16, 256, 1), (0, 0, 1, 128, 1), (0, 0, 1, 768, 1), (0, 0, 1, 256, 0), (0, 0, 1, 256, 33),
+                 (0, 2, 8, 1024, 9)):
+        op, sc, d, blk, bpc = args
+        assert L.hrs_probe_stream(op, p16, p16, 1024, sc, d, 1, blk, bpc, None) != ok, args
+    assert L.hrs_probe_stream(0, None, p16, 1024, 0, 1, 1, 256, 1, None) != ok  # copy without a source
+    assert L.hrs_probe_stream(2, None, None, 1024, 0, 1, 1, 256, 1, None) != ok  # write without a destination
+    einval = L.hrs_probe_stream(0, p16, p16, 1024, 0, 3, 1, 256, 1, None)
+    ealign = L.hrs_probe_stream(0, p16 + 1, p16, 1024, 0, 1, 1, 256, 1, None)
     assert ealign not in (ok, einval)
-    assert L.hrs_probe_stream(0, p16, p16, 1000, 1, 1, 1, None) == ealign  # bytes % 16
-    assert L.hrs_probe_stream(1, p16, p16, 0, 8, 0, 4, None) == ok  # nothing to move: no launch
+    assert L.hrs_probe_stream(0, p16, p16, 1000, 0, 1, 1, 256, 1, None) == ealign  # bytes % 16
+    assert L.hrs_probe_stream(1, p16, p16, 0, 2, 8, 0, 1024, 1, None) == ok  # nothing to move: no launch
 
 
 def test_rows_argument_checks():
-    L = _lib.lib()
+    L = _lib.probe_lib()
     buf = ctypes.create_string_buffer(4096)
     p16 = (ctypes.addressof(buf) + 15) & ~15
     einval = L.hrs_probe_rows(p16, 1, 14, 2048, 11, 4, 0, 2, None)  # 11 + 4 > 14
@@ -45,19 +49,22 @@ def test_rows_argument_checks():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk", [1, 2, 4, 8])
+@pytest.mark.parametrize("schedule", [device.WAVE_TASKS, device.GRID_STRIDE, device.BLOCK_RANGE])
+@pytest.mark.parametrize("depth", [1, 2, 4, 8])
 @pytest.mark.parametrize("nt", [True, False])
-def test_stream_shapes_move_every_byte(cuda, chunk, nt):
+@pytest.mark.parametrize("block,bpc", [(256, 2), (1024, 1)])
+def test_stream_shapes_move_every_byte(cuda, schedule, depth, nt, block, bpc):
     torch = cuda
-    nbytes = (5 << 20) + 48 * 16  # not a whole number of chunks: the tail path runs too
+    nbytes = (5 << 20) + 48 * 16  # not a whole number of tasks / groups: the tail paths run too
     src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
     dst = torch.zeros_like(src)
-    device.probe_copy(src, dst, 2, chunk, nt)
+    kw = dict(schedule=schedule, depth=depth, nontemporal=nt, block_threads=block, blocks_per_cu=bpc)
+    device.probe_copy(src, dst, **kw)
     assert torch.equal(dst, src)
     sink = torch.zeros(4096, dtype=torch.uint8, device="cuda")
-    device.probe_read(src, sink, 1, chunk, nt)
+    device.probe_read(src, sink, **kw)
     dst.zero_()
-    device.probe_write(dst, 4, chunk, nt)
+    device.probe_write(dst, **kw)
     torch.cuda.synchronize()
     assert int(sink.sum().item()) == 0
     w = dst.view(torch.int32).view(-1, 4)  # 16-byte elements as 4 words
