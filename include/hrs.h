@@ -225,6 +225,14 @@ hrs_status hrs_collect(hrs_codec* codec, uint64_t ticket, uint8_t* const* output
  * caller's output rows: the JNI shim calls it outside any
  * GetPrimitiveArrayCritical region. HRS_EINVAL for an unknown ticket. */
 hrs_status hrs_wait(hrs_codec* codec, uint64_t ticket);
+/* Drops an uncollected operation without copying anything out: its slot's
+ * stream is drained (whatever state its GPU work ended in) and the slot
+ * freed for the next submit. For a binding that gives up on a round — the
+ * JNI shim calls it when hrs_wait fails, before the IOException reaches
+ * Java, so a caller that treats the exception as final does not lose one of
+ * the handle's 4 slots. HRS_EINVAL for an unknown ticket; the drain's HIP
+ * error if it fails (the slot is freed either way). */
+hrs_status hrs_release(hrs_codec* codec, uint64_t ticket);
 /* Uncollected operations of this handle. */
 int hrs_pending(const hrs_codec* codec);
 /* Shape of an uncollected operation: output rows, their length, CRC values

@@ -185,6 +185,9 @@ class HipCode : public ErasureCode {
   // only copies.
   void wait(uint64_t ticket) { check(hrs_wait(h_, ticket), h_); }
 
+  // Drop an uncollected operation (its slot is drained and freed).
+  void release(uint64_t ticket) { check(hrs_release(h_, ticket), h_); }
+
   // outputs must hold the operation's output rows exactly, and *crcs (a
   // checksummed operation only) its CRC values: hrs_collect writes that many.
   void collect(uint64_t ticket, const std::vector<uint8_t*>& outputs, std::vector<uint32_t>* crcs) {

@@ -40,7 +40,7 @@ EXPORTS = (
     "hrs_encode_dev", "hrs_decode_dev", "hrs_decode_batch_dev", "hrs_apply_dev", "hrs_crc32_dev",
     "hrs_encode_crc_dev", "hrs_decode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
-    "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_wait",
+    "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_wait", "hrs_release",
 )
 # include/hrs_probe.h, exported by libhrs_probe.so
 PROBE_EXPORTS = ("hrs_probe_stream", "hrs_probe_rows")
@@ -109,6 +109,7 @@ def lib():
         "hrs_collect": ([P, ctypes.c_uint64, PP, P], I),
         "hrs_pending": ([P], I),
         "hrs_wait": ([P, ctypes.c_uint64], I),
+        "hrs_release": ([P, ctypes.c_uint64], I),
         "hrs_ticket_shape": ([P, ctypes.c_uint64, IP, ctypes.POINTER(ctypes.c_size_t), IP], I),
         "hrs_set_kernel_mode": ([P, I], I),
         "hrs_last_kernel": ([P], ctypes.c_char_p),

@@ -219,7 +219,7 @@ size_t hbatch_target_bytes() {
 // interleave both: tools/bench_hbatch.py).
 bool hbatch_duplex() {
   const char* e = getenv("HRS_HBATCH_DUPLEX");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 hrs_status hbatch_slot(hrs_codec* c, int i, size_t dev_bytes, size_t pin_bytes) {

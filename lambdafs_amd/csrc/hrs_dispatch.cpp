@@ -206,9 +206,12 @@ hrs_status crc_window_tables(hrs_codec* c) {
 
 // Fold tables for rows of `len` bytes cut in windows of `win` bytes (32 KiB,
 // or a smaller fused window), keyed by (len, win). At most kFoldCacheMax
-// entries; a new key evicts the least recently used one, after the event
-// recorded behind its latest fold launch (crc_fold) has completed — never a
-// device-wide sync, so other streams' work and other handles are not stalled.
+// entries; a new key evicts the least recently used one once the event
+// recorded behind its latest fold launch has completed. Uses of one table
+// are chained like the raw-CRC scratch (crc_fold: a fold first waits, on the
+// GPU, for the table's previous use, whatever stream that ran on), so that
+// event covers every fold that read the table. The host waits only for it
+// (hipFree itself may still synchronize the device).
 constexpr size_t kFoldCacheMax = 64;
 
 hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, uint64_t win, hrs_codec::FoldTables** out) {
@@ -303,6 +306,10 @@ hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_
   hrs_status st = crc_fold_tables(c, len, win, &ft);
   if (st != HRS_OK) return st;
   const uint32_t* fold = ft->dev;
+  if (ft->used) {  // chain the table's uses: last_use then covers all of them
+    hipError_t e = hipStreamWaitEvent(s, ft->last_use, 0);
+    if (e != hipSuccess) return hip_fail(c, e, "hipStreamWaitEvent");
+  }
   hrs::CrcFoldArgs f{};
   f.raw = raw;
   f.nwin = len / win;
@@ -314,7 +321,7 @@ hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_
   f.crc_out = crc_out;
   hipError_t e = hrs::launch_crc_fold(f, hrs::device_cu_count(), s);
   if (e != hipSuccess) return hip_fail(c, e, "crc fold launch");
-  e = hipEventRecord(ft->last_use, s);  // the tables may be freed once this fold has run
+  e = hipEventRecord(ft->last_use, s);  // the tables may be freed once this fold (and every earlier one) has run
   if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   ft->used = true;
   return HRS_OK;

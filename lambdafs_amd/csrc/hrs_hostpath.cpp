@@ -462,6 +462,23 @@ hrs_status hrs_wait(hrs_codec* c, uint64_t ticket) {
   return fail(c, HRS_EINVAL, "no uncollected operation with ticket %llu", static_cast<unsigned long long>(ticket));
 }
 
+hrs_status hrs_release(hrs_codec* c, uint64_t ticket) {
+  if (!c) return HRS_EINVAL;
+  for (auto& s : c->async)
+    if (s.busy && s.ticket == ticket) {
+      hrs_status st = HRS_OK;
+      if (s.queued) {  // nothing of this round may still read or write the slot's staging
+        DeviceGuard g(c->device);
+        const hipError_t e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess) st = hip_fail(c, e, "hipStreamSynchronize");
+      }
+      s.busy = false;
+      s.queued = false;
+      return st;
+    }
+  return fail(c, HRS_EINVAL, "no uncollected operation with ticket %llu", static_cast<unsigned long long>(ticket));
+}
+
 hrs_status hrs_ticket_shape(const hrs_codec* c, uint64_t ticket, int* num_outputs, size_t* len, int* num_crcs) {
   if (!c) return HRS_EINVAL;
   for (const auto& s : c->async)

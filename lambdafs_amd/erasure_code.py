@@ -459,6 +459,11 @@ class _HipErasureCode(ErasureCode):
         collecting it (hrs_wait; collect then returns without blocking)."""
         self._check(_lib.lib().hrs_wait(self._handle(), int(ticket)))
 
+    def release(self, ticket):
+        """Drop a submitted operation without collecting it (hrs_release): its
+        slot is drained and freed."""
+        self._check(_lib.lib().hrs_release(self._handle(), int(ticket)))
+
     def pending(self):
         """Submitted operations not yet collected (at most 4 per codec)."""
         return int(_lib.lib().hrs_pending(self._handle()))

@@ -513,7 +513,11 @@ JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_collect(JNIEnv* en
   {
     const hrs_status ws = hrs_wait(c, (uint64_t)ticket);
     if (ws != HRS_OK) {
+      /* the round failed: throw, then drain and free its slot (hrs_release),
+       * so a caller that treats the IOException as final does not lose one
+       * of the handle's 4 slots with its copies possibly still in flight */
       throw_status(env, ws, c);
+      (void)hrs_release(c, (uint64_t)ticket);
       return;
     }
   }

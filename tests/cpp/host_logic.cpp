@@ -152,6 +152,16 @@ void rs_checks(int k, int p) {
   expect(hrs_collect(c, z[2], outs.data(), crc.data()) == HRS_EINVAL, "a ticket collects once");
   for (int i : {0, 1, 3}) expect(hrs_collect(c, z[i], outs.data(), crc.data()) == HRS_OK, "collect the rest");
   expect(hrs_pending(c) == 0 && hrs_ticket_shape(c, z[0], nullptr, nullptr, nullptr) == HRS_EINVAL, "all collected");
+  // hrs_release drops an uncollected operation and frees its slot
+  for (auto& zt : z) zt = 0;
+  taken = 0;
+  for (int i = 0; i < 4; ++i) taken += hrs_encode_submit(c, rows.data(), 0, 0, &z[i]) == HRS_OK;
+  expect(taken == 4 && hrs_release(c, z[1]) == HRS_OK && hrs_pending(c) == 3, "release frees a slot");
+  expect(hrs_release(c, z[1]) == HRS_EINVAL && hrs_collect(c, z[1], outs.data(), nullptr) == HRS_EINVAL,
+         "a released ticket is gone");
+  expect(hrs_encode_submit(c, rows.data(), 0, 0, &z[4]) == HRS_OK && hrs_pending(c) == 4, "its slot is reusable");
+  for (int i : {0, 2, 3, 4}) expect(hrs_release(c, z[i]) == HRS_OK, "release the rest");
+  expect(hrs_pending(c) == 0 && hrs_release(nullptr, 1) == HRS_EINVAL, "all released");
   hrs_destroy(c);
 }
 

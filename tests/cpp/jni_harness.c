@@ -299,10 +299,15 @@ static void JNICALL f_SetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, j
  * i.e. that no critical region covers a GPU wait. */
 static uint64_t g_waited_ticket = 0;
 static uint64_t g_collect_ticket = 0; /* nonzero while a collect call runs */
+static int g_fail_wait = 0;           /* the next hrs_wait reports a device error */
 hrs_status hrs_wait(hrs_codec* c, uint64_t t) {
   static hrs_status (*real)(hrs_codec*, uint64_t) = NULL;
   if (!real) *(void**)&real = dlsym(RTLD_NEXT, "hrs_wait");
   g_waited_ticket = t;
+  if (g_fail_wait) {
+    g_fail_wait = 0;
+    return HRS_EDEVICE;
+  }
   return real ? real(c, t) : HRS_EDEVICE;
 }
 
@@ -779,6 +784,20 @@ static int gpu_checks(void) {
     EXPECT_THROWN("fifth outstanding round", kIAE, t5[4] = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
     for (int r = 3; r >= 0; --r) COLLECT("collect out of order", t5[r], rows(p, 4096, 0), NULL);
     expect(!vm.pending, "collect in any order");
+    /* a collect whose wait fails throws IOException AND frees the
+     * round's slot (hrs_release), so the handle keeps its 4 slots */
+    jlong tf = 0;
+    CALL("encodeSubmit (wait fails)", tf = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
+    g_fail_wait = 1;
+    g_collect_ticket = (uint64_t)tf;
+    EXPECT_THROWN("collect after a failed wait", kIOE, NS(collect)(env, NULL, h, tf, rows(p, 4096, 0), NULL));
+    g_collect_ticket = 0;
+    jint pend_f = -1;
+    CALL("pending after the failed collect", pend_f = NS(pending)(env, NULL, h));
+    expect(pend_f == 0, "a failed collect releases its slot (pending %d)", (int)pend_f);
+    for (int r = 0; r < 4; ++r) CALL("encodeSubmit x4 again", t5[r] = NS(encodeSubmit)(env, NULL, h, in, 4096, JNI_FALSE));
+    expect(!vm.pending, "all 4 slots usable after the failed collect");
+    for (int r = 0; r < 4; ++r) COLLECT("collect x4 again", t5[r], rows(p, 4096, 0), NULL);
   }
   CALL("destroy", NS(destroy)(env, NULL, h));
 

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 from lambdafs_amd import HipReedSolomonCode, device
+from oracle import rs_oracle as C
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -86,6 +87,37 @@ def test_encode_then_block_checksums(cuda):
     for s in (0, S - 1):
         for r in range(k + p):
             assert _u32(crcs[s, r]) == zlib.crc32(host[s, r].tobytes())
+
+
+@pytest.mark.gpu
+def test_fold_table_shared_by_slot_streams_survives_eviction(cuda):
+    """two asynchronous checksummed encodes of the same row length
+    run their folds on two different slot streams with one fold table; 64
+    device CRC calls of other lengths then evict that table while both may
+    still be queued. Uses of a table are chained (each fold waits for the
+    previous one), so the eviction waits for both folds. Every CRC vs zlib."""
+    torch = cuda
+    k, p, L = 10, 4, (256 << 10) + 40
+    code = HipReedSolomonCode(k, p)
+    rng = np.random.default_rng(78)
+    rounds = [[rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] for _ in range(2)]
+    keep = [[r.copy() for r in rnd] for rnd in rounds]
+    tickets = [code.encodeBulkAsync(rnd, checksums=True) for rnd in rounds]
+    side = []
+    for i in range(66):
+        Li = 8192 + 64 * i
+        rows = torch.from_numpy(rng.integers(0, 256, (2, Li), dtype=np.uint8)).cuda()
+        side.append((rows, device.crc32_rows(code, [rows[r:r + 1] for r in range(2)])))
+    for t, kept in zip(tickets, keep):
+        out = [np.zeros(L, np.uint8) for _ in range(p)]
+        crcs = code.collect(t, out)
+        ref = C.encode_bulk(k, p, [x.copy() for x in kept])
+        assert all(np.array_equal(o, r) for o, r in zip(out, ref))
+        assert crcs == [zlib.crc32(b.tobytes()) for b in kept + list(ref)]
+    torch.cuda.synchronize()
+    for rows, got in side:
+        host = rows.cpu().numpy()
+        assert [int(x) & 0xFFFFFFFF for x in got[0].tolist()] == [zlib.crc32(host[r].tobytes()) for r in range(2)]
 
 
 @pytest.mark.gpu
