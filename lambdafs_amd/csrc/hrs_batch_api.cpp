@@ -16,6 +16,7 @@
 #include "hrs_codec.hpp"
 #include "hrs_host.hpp"
 #include "hrs_internal.hpp"
+#include "hrs_launch.hpp"
 
 namespace hrs::api {
 
@@ -204,6 +205,28 @@ bool is_pinned(const void* p) {
   return attr.type == hipMemoryTypeHost;
 }
 
+bool zero_copy_on() {
+  const char* e = getenv("HRS_ZEROCOPY");
+  return !(e && e[0] == '0');
+}
+
+unsigned zero_copy_blocks() {
+  const char* e = getenv("HRS_ZC_BLOCKS");
+  const long x = e ? atol(e) : 0;
+  return x > 0 ? static_cast<unsigned>(x) : 0u;
+}
+
+bool host_device_ptr(const void* p, uint8_t** dp) {
+  if (!p || !is_pinned(p)) return false;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    return false;
+  }
+  *dp = static_cast<uint8_t*>(d);
+  return true;
+}
+
 size_t hbatch_target_bytes() {
   static const size_t v = [] {
     const char* e = getenv("HRS_HBATCH_BYTES");
@@ -322,10 +345,18 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
   const bool pinned = is_pinned(hin) && is_pinned(hout);
   const size_t dev_bytes = chunk * (img_stripe + out_stripe_dev);
   const size_t pin_bytes = pinned ? 0 : dev_bytes;  // staging mirrors the device image
+  // pageable callers, zero copy: the kernels read each chunk's image from the
+  // slot's pinned staging and write its outputs there (no device image, no
+  // H2D / D2H); the host copies in and out of staging as before
+  const bool zc = !pinned && zero_copy_on();
   for (int i = 0; i < hrs::kHostBatchSlots; ++i) {
-    hrs_status st = hbatch_slot(c, i, dev_bytes, pin_bytes);
+    hrs_status st = hbatch_slot(c, i, zc ? 0 : dev_bytes, pin_bytes);
     if (st != HRS_OK) return st;
   }
+  uint8_t* zc_img[hrs::kHostBatchSlots] = {};
+  for (int i = 0; i < hrs::kHostBatchSlots && zc; ++i)
+    if (!host_device_ptr(c->hbatch[i].pin, &zc_img[i])) return fail(c, HRS_EDEVICE, "staging not device-mapped");
+  hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
   const bool duplex = hbatch_duplex();
@@ -373,9 +404,19 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
     // stream of each stage; in duplex mode the H2D waits until the slot's
     // previous kernels have read its image, the kernels until the previous
     // D2H has read its output block, the D2H until this chunk's kernels
+    hipError_t e = hipSuccess;
+    if (zc) {  // the kernels work on the staging itself
+      uint8_t* zimg = zc_img[sl];
+      hrs_status st = compute(h.stream, s0, ns, zimg, img_stripe, dpitch, zimg + chunk * img_stripe, out_stripe_dev);
+      if (st != HRS_OK) return st;
+      if ((e = hipEventRecord(h.done, h.stream)) != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+      pend[sl].busy = pend[sl].used = true;
+      pend[sl].s0 = s0;
+      pend[sl].ns = ns;
+      continue;
+    }
     const hipStream_t s_in = duplex ? c->hbatch_in : h.stream;
     const hipStream_t s_out = duplex ? c->hbatch_out : h.stream;
-    hipError_t e = hipSuccess;
     if (duplex && pend[sl].used && (e = hipStreamWaitEvent(s_in, h.comp_done, 0)) != hipSuccess)
       return hip_fail(c, e, "hipStreamWaitEvent");
     uint8_t* dimg = h.dev;
@@ -427,6 +468,38 @@ hrs_status drain_hbatch(hrs_codec* c, hrs_status st) {
       if (h.stream) (void)hipStreamSynchronize(h.stream);
   }
   return st;
+}
+
+// hrs_decode_batch_host with pinned stripes and outputs: one batch launch
+// whose kernels read the survivors and write the repaired cells across the
+// host link directly (zero copy). The plans go up first on slot 0's stream;
+// the call returns once the launch has completed.
+hrs_status zero_copy_batch(hrs_codec* c, const BatchPlanSet& ps, const uint8_t* ds, size_t row_stride,
+                           size_t stripe_stride, uint8_t* dout, size_t out_row_stride, size_t out_stripe_stride,
+                           size_t len, size_t nstripes) {
+  hrs_status st = hbatch_slot(c, 0, 0, 0);
+  if (st != HRS_OK) return st;
+  const hipStream_t hs = c->hbatch[0].stream;
+  hrs_codec::BatchSlot* bsl = nullptr;
+  const hrs::BatchPlan* dplans = nullptr;
+  const int32_t* dpat = nullptr;
+  if (ps.fused) {
+    st = upload_batch_plans(c, ps, hs, &bsl, &dplans, &dpat);
+    if (st != HRS_OK) return st;
+  }
+  {
+    hrs::GridCap cap(zero_copy_blocks());
+    st = launch_batch(c, ps, dplans, dpat, ds, row_stride, stripe_stride, dout, out_row_stride, out_stripe_stride,
+                      len, 0, nstripes, hs);
+  }
+  if (st != HRS_OK) return st;
+  if (bsl) {
+    const hipError_t e = hipEventRecord(bsl->done, hs);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+    bsl->pending = true;
+  }
+  const hipError_t e = hipStreamSynchronize(hs);
+  return e == hipSuccess ? HRS_OK : hip_fail(c, e, "hipStreamSynchronize");
 }
 
 }  // namespace hrs::api
@@ -481,6 +554,10 @@ hrs_status hrs_decode_batch_host(hrs_codec* c, const uint8_t* stripes, size_t ro
   if (ps.max_nout == 0) return HRS_OK;
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
+  uint8_t *zs = nullptr, *zo = nullptr;
+  if (zero_copy_on() && host_device_ptr(stripes, &zs) && host_device_ptr(out, &zo))
+    return drain_hbatch(c, zero_copy_batch(c, ps, zs, row_stride, stripe_stride, zo, out_row_stride,
+                                           out_stripe_stride, len, nstripes));
   // rows each pattern reads: its live locations (every location for the
   // per-stripe fallback of wide patterns, which reads what its matrix needs)
   std::vector<std::vector<RowRun>> pruns(ps.plans.size());
@@ -542,6 +619,26 @@ hrs_status hrs_encode_batch_host(hrs_codec* c, uint8_t* stripes, size_t row_stri
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   const int k = c->k, p = c->p;
+  uint8_t* zs = nullptr;
+  if (zero_copy_on() && host_device_ptr(stripes, &zs)) {  // pinned: the kernel works on the caller's stripes
+    hrs_status st = hbatch_slot(c, 0, 0, 0);
+    if (st != HRS_OK) return st;
+    const hipStream_t hs = c->hbatch[0].stream;
+    std::vector<const uint8_t*> in(k);
+    std::vector<uint8_t*> outp(p);
+    for (int i = 0; i < k; ++i) in[i] = zs + static_cast<size_t>(p + i) * row_stride;
+    for (int r = 0; r < p; ++r) outp[r] = zs + static_cast<size_t>(r) * row_stride;
+    {
+      hrs::GridCap cap(zero_copy_blocks());
+      st = run_apply(c, c->g.data(), p, k, in.data(), stripe_stride, outp.data(), stripe_stride, len, nstripes, hs,
+                     static_encode_family(c));
+    }
+    if (st == HRS_OK) {
+      const hipError_t e = hipStreamSynchronize(hs);
+      if (e != hipSuccess) st = hip_fail(c, e, "hipStreamSynchronize");
+    }
+    return drain_hbatch(c, st);
+  }
   const std::vector<RowRun> data_rows{{p, k}};  // hops locations p..n-1: one run
   auto reads = [&](size_t) -> const std::vector<RowRun>& { return data_rows; };
   auto writes = [&](size_t) -> int { return p; };

@@ -135,6 +135,17 @@ struct DeviceGuard {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// ---- zero copy (hrs_batch_api.cpp): kernels read and write pinned host
+// memory across the host link directly instead of H2D -> kernel -> D2H — the
+// link then carries both directions at once with no copy-engine calls
+// (profiles/r04/NOTES.md). HRS_ZEROCOPY=0 turns it off (A/B runs; read per
+// call); HRS_ZC_BLOCKS caps the grid of such launches (hrs::GridCap).
+bool zero_copy_on();
+unsigned zero_copy_blocks();
+// Device address of pinned host memory (hipHostMalloc'd or registered), or
+// false for pageable memory.
+bool host_device_ptr(const void* p, uint8_t** dp);
+
 // The compile-time encode kernels hold the hops RS generator (rs) or the
 // ISA-L Cauchy rows (nrs) of a (k, p) shape; only those families' G may take
 // them. SRC's G (XOR groups over RS(k, r)) and XOR's all-ones row may not.

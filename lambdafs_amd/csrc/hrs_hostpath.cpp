@@ -16,6 +16,7 @@
 #include "crc32.hpp"
 #include "hrs_host.hpp"
 #include "hrs_internal.hpp"
+#include "hrs_launch.hpp"
 
 namespace hrs::api {
 
@@ -112,6 +113,14 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     hrs_status st = host_slot(c, i, need);
     if (st != HRS_OK) return st;
   }
+  // zero copy (no checksums): the kernel reads the chunk from the slot's
+  // pinned staging and writes its outputs there, across the host link — no
+  // H2D / D2H (checksummed calls keep the device copy: their CRC pass would
+  // read the cells across the link a second time)
+  uint8_t* zpin[2] = {nullptr, nullptr};
+  const bool zc = ncrc == 0 && zero_copy_on() && host_device_ptr(c->host[0].pin, &zpin[0]) &&
+                  host_device_ptr(c->host[1].pin, &zpin[1]);
+  hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
   size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
@@ -144,12 +153,13 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     for (int i = 0; i < nin; ++i)
       if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
     pool.run(jobs);
-    if (nlive > 0) {
+    if (nlive > 0 && !zc) {
       hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
       if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
     }
-    for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? h.dev + pitch * slot_of[i] : nullptr;
-    for (int o = 0; o < nout; ++o) dout[o] = h.dev + pitch * (nlive + o);
+    uint8_t* img = zc ? zpin[sl] : h.dev;
+    for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
+    for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
     uint32_t* dcrc = reinterpret_cast<uint32_t*>(h.dev + crc_off);
     uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
     if (crc.mode == kCrcEncode)
@@ -161,8 +171,11 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     if (st != HRS_OK) return st;
     // outputs (and the chunk CRCs right behind them) back to the staging
     const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + lj;
-    hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost, h.stream);
-    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+    hipError_t e = hipSuccess;
+    if (!zc) {
+      e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost, h.stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+    }
     e = hipEventRecord(h.done, h.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
     pending[sl] = true;
@@ -242,14 +255,18 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
   for (int i = 0; i < nin; ++i)
     if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len});
   hrs::CopyPool::instance().run(jobs);
-  if (nlive > 0) {
+  uint8_t* zpin = nullptr;  // zero copy, as host_apply_impl
+  const bool zc = ncrc == 0 && zero_copy_on() && host_device_ptr(a.pin, &zpin);
+  hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
+  if (nlive > 0 && !zc) {
     hipError_t e = hipMemcpyAsync(a.dev, a.pin, pitch * (nlive - 1) + len, hipMemcpyHostToDevice, a.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
   }
   std::vector<const uint8_t*> din(nin);
   std::vector<uint8_t*> dout(nout);
-  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? a.dev + pitch * slot_of[i] : nullptr;
-  for (int o = 0; o < nout; ++o) dout[o] = a.dev + pitch * (nlive + o);
+  uint8_t* img = zc ? zpin : a.dev;
+  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
+  for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
   uint32_t* dcrc = reinterpret_cast<uint32_t*>(a.dev + crc_off);
   uint32_t* draw = reinterpret_cast<uint32_t*>(a.dev + raw_off);
   if (crc_mode == kCrcEncode)
@@ -260,8 +277,11 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
     st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, a.stream, static_kp);
   if (st != HRS_OK) return st;
   const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + len;
-  hipError_t e = hipMemcpyAsync(a.pin + pitch * nlive, a.dev + pitch * nlive, back, hipMemcpyDeviceToHost, a.stream);
-  if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+  hipError_t e = hipSuccess;
+  if (!zc) {
+    e = hipMemcpyAsync(a.pin + pitch * nlive, a.dev + pitch * nlive, back, hipMemcpyDeviceToHost, a.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+  }
   e = hipEventRecord(a.done, a.stream);
   if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   a.nout = nout;

@@ -60,11 +60,28 @@ inline int blocks_per_cu(int dflt = 2) {
   return v ? v : dflt;
 }
 
+// Zero-copy launches (kernels reading and writing pinned host memory across
+// the host link, hrs_batch_api.cpp / hrs_hostpath.cpp) cap their grid: the
+// link, not the CUs, bounds them, so a capped grid leaves the rest of the chip
+// to other work. Set for the calling thread by a GridCap around the launch.
+inline thread_local unsigned t_grid_cap = 0;
+
+struct GridCap {
+  unsigned prev;
+  explicit GridCap(unsigned cap) : prev(t_grid_cap) { t_grid_cap = cap; }
+  ~GridCap() { t_grid_cap = prev; }
+};
+
+inline unsigned capped_grid(uint64_t g) {
+  if (t_grid_cap && g > t_grid_cap) g = t_grid_cap;
+  return static_cast<unsigned>(g == 0 ? 1 : g);
+}
+
 inline unsigned stream_grid(uint64_t ntasks, int per_cu = 2) {
   const uint64_t want = static_cast<uint64_t>(blocks_per_cu(per_cu)) * device_cus();
   const uint64_t needed = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
   uint64_t g = needed < want ? needed : want;
-  return static_cast<unsigned>(g == 0 ? 1 : g);
+  return capped_grid(g);
 }
 
 template <typename Kernel>
@@ -76,8 +93,7 @@ inline unsigned grid_for(Kernel kernel, uint64_t work_items_per_block, uint64_t 
   const uint64_t resident = static_cast<uint64_t>(per_cu) * device_cus();
   const uint64_t needed = (ntasks + work_items_per_block - 1) / work_items_per_block;
   uint64_t g = needed < resident ? needed : resident;
-  if (g == 0) g = 1;
-  return static_cast<unsigned>(g);
+  return capped_grid(g);
 }
 
 }  // namespace hrs

@@ -1,6 +1,11 @@
 """Host-memory batch pipelines (hrs_decode_batch_host / hrs_encode_batch_host)
-A/B: H2D and D2H on per-direction streams (duplex, default) vs on each slot's
-stream (HRS_HBATCH_DUPLEX=0, round 3), interleaved rep by rep in one process.
+A/B, interleaved rep by rep in one process:
+  ring     H2D -> kernel -> D2H on each slot's stream (round 3; HRS_ZEROCOPY=0)
+  duplex   H2D / D2H on per-direction streams (HRS_ZEROCOPY=0 HRS_HBATCH_DUPLEX=1)
+  zc       zero copy: the kernels read and write the pinned host memory itself
+           (pinned callers: one launch over the caller's stripes; pageable:
+           over the slots' pinned staging), default
+  zc_bN    zc with the grid capped at N blocks (HRS_ZC_BLOCKS=N)
 Workload = BASELINE configs[4] per GPU: RS(12,4), 256 KiB cells, 512 stripes,
 a seeded random lost pair per stripe; pinned and pageable host memory.
 
@@ -29,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stripes", type=int, default=512)
+    ap.add_argument("--zc-blocks", type=int, nargs="*", default=[512, 256, 128, 64])
     args = ap.parse_args()
     k, p, L, S = 12, 4, 256 << 10, args.stripes
     n = k + p
@@ -48,18 +54,27 @@ def main():
     pout = np.zeros((S, 2, L), np.uint8)
     idx = np.arange(S)[:, None]
     want = ref.numpy()[idx, er]
+    pge = np.array(stn)
     legs = {
         "decode_pinned": lambda: device.decode_batch_host(code, stn, er, outn),
         "decode_pageable": lambda: device.decode_batch_host(code, pg, er, pout),
         "encode_pinned": lambda: device.encode_batch_host(code, stn),
+        "encode_pageable": lambda: device.encode_batch_host(code, pge),
     }
-    res = {m: {leg: [] for leg in legs} for m in ("duplex", "serial")}
+    modes = {"ring": {"HRS_ZEROCOPY": "0"}, "duplex": {"HRS_ZEROCOPY": "0", "HRS_HBATCH_DUPLEX": "1"}, "zc": {}}
+    for b in args.zc_blocks:
+        modes[f"zc_b{b}"] = {"HRS_ZC_BLOCKS": str(b)}
+    res = {m: {leg: [] for leg in legs} for m in modes}
     for r in range(args.reps + 1):
-        for m in ("duplex", "serial"):
-            os.environ["HRS_HBATCH_DUPLEX"] = "1" if m == "duplex" else "0"
+        for m, env in modes.items():
+            for key in ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS"):
+                os.environ.pop(key, None)
+            os.environ.update(env)
             for leg, fn in legs.items():
-                if leg.startswith("encode"):
+                if leg == "encode_pinned":
                     stn[:, :p] = 0
+                if leg == "encode_pageable":
+                    pge[:, :p] = 0
                 t0 = time.perf_counter()
                 fn()
                 dt = (time.perf_counter() - t0) * 1e3
@@ -67,12 +82,14 @@ def main():
                     res[m][leg].append(dt)
                 ok = (np.array_equal(outn, want) if leg == "decode_pinned" else
                       np.array_equal(pout, want) if leg == "decode_pageable" else
-                      np.array_equal(stn, ref.numpy()))
+                      np.array_equal(stn, ref.numpy()) if leg == "encode_pinned" else
+                      np.array_equal(pge, ref.numpy()))
                 if not ok:
                     raise RuntimeError(f"{m} {leg}: output differs")
                 outn[:] = 0
                 pout[:] = 0
-    os.environ.pop("HRS_HBATCH_DUPLEX")
+    for key in ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS"):
+        os.environ.pop(key, None)
     line = {"workload": f"RS({k},{p}) {L >> 10} KiB cells x {S} stripes, random lost pair per stripe",
             "bit_exact": True}
     for m in res:
@@ -81,8 +98,9 @@ def main():
             line[f"{m}_{leg}_ms"] = round(med, 3)
             line[f"{m}_{leg}_min_ms"] = round(float(np.min(v)), 3)
             line[f"{m}_{leg}_GiBps_user"] = round(k * L * S / GiB / (med * 1e-3), 2)
-    for leg in legs:
-        line[f"gain_{leg}"] = round(line[f"serial_{leg}_ms"] / line[f"duplex_{leg}_ms"], 3)
+    for m in modes:
+        for leg in legs:
+            line[f"gain_{m}_vs_ring_{leg}"] = round(line[f"ring_{leg}_ms"] / line[f"{m}_{leg}_ms"], 3)
     print(json.dumps(line), flush=True)
 
 
