@@ -160,9 +160,9 @@ void hrs_destroy(hrs_codec* c) {
   }
   if (c->crc_tables_a) (void)hipFree(c->crc_tables_a);
   for (auto& kv : c->crc_fold_tables) {
-    if (kv.second.last_use) {
-      (void)hipEventSynchronize(kv.second.last_use);
-      (void)hipEventDestroy(kv.second.last_use);
+    for (auto& u : kv.second.uses) {
+      (void)hipEventSynchronize(u.ev);
+      (void)hipEventDestroy(u.ev);
     }
     (void)hipFree(kv.second.dev);
   }

@@ -210,9 +210,13 @@ bool zero_copy_on() {
   return !(e && e[0] == '0');
 }
 
+// 64 blocks (256 waves) keep the host link as busy as a full grid does:
+// config 5's repair 28.99 ms at 64 vs 29.66 uncapped, its encode 28.55 vs
+// 29.57 (tools/bench_hbatch.py, profiles/r04/d/) — and leave 3/4 of the chip
+// free for other work. HRS_ZC_BLOCKS=0 lifts the cap.
 unsigned zero_copy_blocks() {
   const char* e = getenv("HRS_ZC_BLOCKS");
-  const long x = e ? atol(e) : 0;
+  const long x = e ? atol(e) : 64;
   return x > 0 ? static_cast<unsigned>(x) : 0u;
 }
 
@@ -277,9 +281,11 @@ hrs_status hbatch_slot(hrs_codec* c, int i, size_t dev_bytes, size_t pin_bytes) 
     (void)hipStreamSynchronize(h.stream);
     if (h.pin) (void)hipHostFree(h.pin);
     h.pin = nullptr;
+    h.pin_dev = nullptr;
     h.pin_bytes = 0;
     hipError_t e = hipHostMalloc(&h.pin, pin_bytes, hipHostMallocDefault);
     if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", pin_bytes, hipGetErrorString(e));
+    if (!host_device_ptr(h.pin, &h.pin_dev)) h.pin_dev = nullptr;
     h.pin_bytes = pin_bytes;
   }
   return HRS_OK;
@@ -348,14 +354,17 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
   // pageable callers, zero copy: the kernels read each chunk's image from the
   // slot's pinned staging and write its outputs there (no device image, no
   // H2D / D2H); the host copies in and out of staging as before
-  const bool zc = !pinned && zero_copy_on();
+  bool zc = !pinned && zero_copy_on();
   for (int i = 0; i < hrs::kHostBatchSlots; ++i) {
     hrs_status st = hbatch_slot(c, i, zc ? 0 : dev_bytes, pin_bytes);
     if (st != HRS_OK) return st;
   }
   uint8_t* zc_img[hrs::kHostBatchSlots] = {};
-  for (int i = 0; i < hrs::kHostBatchSlots && zc; ++i)
-    if (!host_device_ptr(c->hbatch[i].pin, &zc_img[i])) return fail(c, HRS_EDEVICE, "staging not device-mapped");
+  for (int i = 0; i < hrs::kHostBatchSlots && zc; ++i) zc &= (zc_img[i] = c->hbatch[i].pin_dev) != nullptr;
+  for (int i = 0; i < hrs::kHostBatchSlots && !zc && !pinned; ++i) {  // staging not device-mapped: copy engine
+    hrs_status st = hbatch_slot(c, i, dev_bytes, pin_bytes);
+    if (st != HRS_OK) return st;
+  }
   hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;

@@ -34,8 +34,14 @@ struct hrs_codec {
   // event recorded after its latest fold launch has completed
   struct FoldTables {
     uint32_t* dev = nullptr;
-    hipEvent_t last_use = nullptr;
-    bool used = false;
+    // the latest fold that read the tables on each stream that has used them
+    // (slot streams, caller streams): the tables may be freed once every one
+    // of these events has completed
+    struct Use {
+      hipStream_t stream;
+      hipEvent_t ev;
+    };
+    std::vector<Use> uses;
     uint64_t tick = 0;
   };
   std::map<uint64_t, FoldTables> crc_fold_tables;
@@ -60,6 +66,7 @@ struct hrs_codec {
   // its own stream; a slot is reused once its D2H event has completed
   struct HostSlot {
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;  // device address of `pin` (zero-copy kernels)
     uint8_t* dev = nullptr;
     size_t bytes = 0;
     hipStream_t stream = nullptr;
@@ -75,6 +82,7 @@ struct hrs_codec {
     uint8_t* dev = nullptr;
     size_t dev_bytes = 0;
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;  // device address of `pin` (zero-copy kernels)
     size_t pin_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -88,6 +96,7 @@ struct hrs_codec {
   // operation occupies its slot from submit until it is collected
   struct AsyncSlot {
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;  // device address of `pin` (zero-copy kernels)
     uint8_t* dev = nullptr;
     size_t bytes = 0;
     hipStream_t stream = nullptr;

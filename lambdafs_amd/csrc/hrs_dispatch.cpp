@@ -206,12 +206,13 @@ hrs_status crc_window_tables(hrs_codec* c) {
 
 // Fold tables for rows of `len` bytes cut in windows of `win` bytes (32 KiB,
 // or a smaller fused window), keyed by (len, win). At most kFoldCacheMax
-// entries; a new key evicts the least recently used one once the event
-// recorded behind its latest fold launch has completed. Uses of one table
-// are chained like the raw-CRC scratch (crc_fold: a fold first waits, on the
-// GPU, for the table's previous use, whatever stream that ran on), so that
-// event covers every fold that read the table. The host waits only for it
-// (hipFree itself may still synchronize the device).
+// entries; a new key evicts the least recently used one once the latest fold
+// that read it on EVERY stream that used it has completed (FoldTables::uses:
+// one event per stream, re-recorded by each fold on that stream). A table is
+// shared by the handle's slot streams and callers' streams, and no fold waits
+// on another stream's (a cross-stream wait on every fold cost the host-buffer
+// calls up to 2x, profiles/r04/NOTES.md). The host waits only for those
+// events (hipFree itself may still synchronize the device).
 constexpr size_t kFoldCacheMax = 64;
 
 hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, uint64_t win, hrs_codec::FoldTables** out) {
@@ -235,26 +236,54 @@ hrs_status crc_fold_tables(hrs_codec* c, uint64_t len, uint64_t win, hrs_codec::
     for (auto i = c->crc_fold_tables.begin(); i != c->crc_fold_tables.end(); ++i)
       if (i->second.tick < lru->second.tick) lru = i;
     hrs_codec::FoldTables& v = lru->second;
-    if (v.used) {
-      hipError_t e = hipEventSynchronize(v.last_use);
+    for (auto& u : v.uses) {
+      hipError_t e = hipEventSynchronize(u.ev);
       if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
     }
-    if (v.last_use) (void)hipEventDestroy(v.last_use);
+    for (auto& u : v.uses) (void)hipEventDestroy(u.ev);
     (void)hipFree(v.dev);
     c->crc_fold_tables.erase(lru);
   }
   hrs_codec::FoldTables v;
-  hipError_t e = hipEventCreateWithFlags(&v.last_use, hipEventDisableTiming);
-  if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
   hrs_status st = upload(c, h, &v.dev);
   if (st != HRS_OK) {
-    (void)hipEventDestroy(v.last_use);
     if (v.dev) (void)hipFree(v.dev);
     return st;
   }
   v.tick = ++c->crc_fold_tick;
   *out = &(c->crc_fold_tables[key] = v);
   return HRS_OK;
+}
+
+// Records that a fold on stream s read the tables (after its launch). At most
+// kFoldUsesMax streams are tracked per table; a further one first waits for
+// the oldest tracked use and takes over its event.
+constexpr size_t kFoldUsesMax = 32;
+
+hrs_status fold_tables_used(hrs_codec* c, hrs_codec::FoldTables* ft, hipStream_t s) {
+  hrs_codec::FoldTables::Use* u = nullptr;
+  for (auto& x : ft->uses)
+    if (x.stream == s) u = &x;
+  if (!u && ft->uses.size() >= kFoldUsesMax) {  // many caller streams: retire the oldest use
+    hrs_codec::FoldTables::Use old = ft->uses.front();
+    ft->uses.erase(ft->uses.begin());
+    const hipError_t e = hipEventSynchronize(old.ev);
+    if (e != hipSuccess) {
+      (void)hipEventDestroy(old.ev);
+      return hip_fail(c, e, "hipEventSynchronize");
+    }
+    ft->uses.push_back({s, old.ev});
+    u = &ft->uses.back();
+  }
+  if (!u) {
+    hrs_codec::FoldTables::Use nu{s, nullptr};
+    const hipError_t e = hipEventCreateWithFlags(&nu.ev, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+    ft->uses.push_back(nu);
+    u = &ft->uses.back();
+  }
+  const hipError_t e = hipEventRecord(u->ev, s);
+  return e == hipSuccess ? HRS_OK : hip_fail(c, e, "hipEventRecord");
 }
 
 // Raw-CRC scratch of at least `bytes` (the fold reads it after the window
@@ -306,10 +335,6 @@ hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_
   hrs_status st = crc_fold_tables(c, len, win, &ft);
   if (st != HRS_OK) return st;
   const uint32_t* fold = ft->dev;
-  if (ft->used) {  // chain the table's uses: last_use then covers all of them
-    hipError_t e = hipStreamWaitEvent(s, ft->last_use, 0);
-    if (e != hipSuccess) return hip_fail(c, e, "hipStreamWaitEvent");
-  }
   hrs::CrcFoldArgs f{};
   f.raw = raw;
   f.nwin = len / win;
@@ -321,10 +346,7 @@ hrs_status crc_fold(hrs_codec* c, size_t len, uint64_t nsr, const uint32_t* crc_
   f.crc_out = crc_out;
   hipError_t e = hrs::launch_crc_fold(f, hrs::device_cu_count(), s);
   if (e != hipSuccess) return hip_fail(c, e, "crc fold launch");
-  e = hipEventRecord(ft->last_use, s);  // the tables may be freed once this fold (and every earlier one) has run
-  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
-  ft->used = true;
-  return HRS_OK;
+  return fold_tables_used(c, ft, s);  // the tables may be freed once this fold has run
 }
 
 // Sub-windows (2 KiB) per fused window: 16 (32 KiB) when the job has

@@ -13,14 +13,18 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include <sched.h>
 
 namespace hrs {
 
@@ -53,6 +57,7 @@ class CopyPool {
     {
       std::lock_guard<std::mutex> lk(mu_);
       open_.push_back(&b);
+      nopen_.store(open_.size(), std::memory_order_release);
     }
     cv_.notify_all();
     drain(b);
@@ -80,9 +85,29 @@ class CopyPool {
     int users = 0;  // workers inside drain(); guarded by mu_
   };
 
+  // CPUs this process may run on: its affinity set, capped by a cgroup v2 CPU
+  // quota (the GPU boxes give one GPU's job 16 CPUs of a larger machine).
+  static int cpu_share() {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long period = 0;
+      if (fscanf(f, "%31s %ld", q, &period) == 2 && q[0] != 'm' && period > 0) {
+        const long quota = atol(q) / period;
+        if (quota > 0 && (n == 0 || quota < n)) n = static_cast<int>(quota);
+      }
+      fclose(f);
+    }
+    return n > 0 ? n : 2;
+  }
+
   CopyPool() {
     const char* e = getenv("HRS_HOST_THREADS");
-    int n = e ? atoi(e) : 2;  // measured best for one caller on the MI355X hosts (tools/host_sweep.sh)
+    // default: half the CPU share, 2..8 threads (tools/bench_host_ab.py and
+    // bench_hbatch.py sweeps, profiles/r04/NOTES.md)
+    int n = e ? atoi(e) : std::min(8, std::max(2, cpu_share() / 2));
     if (n < 0) n = 0;
     if (n > 32) n = 32;
     nthreads_ = n;
@@ -102,11 +127,25 @@ class CopyPool {
   void close(Batch* b) {  // mu_ held
     auto it = std::find(open_.begin(), open_.end(), b);
     if (it != open_.end()) open_.erase(it);
+    nopen_.store(open_.size(), std::memory_order_release);
+  }
+
+  // A worker that just ran out of work spins this long for the next batch
+  // before it sleeps on the condition variable: a synchronous call posts a
+  // batch every few tens of microseconds (copy-in, then copy-out, per chunk),
+  // and a wake-up through the condition variable costs about as much.
+  static constexpr auto kSpin = std::chrono::microseconds(30);
+
+  void spin_for_work() {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (nopen_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() - t0 < kSpin)
+      __builtin_ia32_pause();
   }
 
   void worker() {
     size_t turn = 0;
     for (;;) {
+      spin_for_work();
       Batch* b = nullptr;
       {
         std::unique_lock<std::mutex> lk(mu_);
@@ -135,6 +174,7 @@ class CopyPool {
   int nthreads_ = 0;
   std::vector<std::thread> threads_;
   std::vector<Batch*> open_;
+  std::atomic<size_t> nopen_{0};  // open_.size(), readable without mu_ (spin_for_work)
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   bool stop_ = false;

@@ -52,11 +52,13 @@ hrs_status host_slot(hrs_codec* c, int i, size_t bytes) {
   if (h.pin) (void)hipHostFree(h.pin);
   h.dev = nullptr;
   h.pin = nullptr;
+  h.pin_dev = nullptr;
   h.bytes = 0;
   hipError_t e = hipMalloc(&h.dev, bytes);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   e = hipHostMalloc(&h.pin, bytes, hipHostMallocDefault);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  if (!host_device_ptr(h.pin, &h.pin_dev)) h.pin_dev = nullptr;  // then the calls take the copy engine
   h.bytes = bytes;
   return HRS_OK;
 }
@@ -117,9 +119,8 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
   // pinned staging and writes its outputs there, across the host link — no
   // H2D / D2H (checksummed calls keep the device copy: their CRC pass would
   // read the cells across the link a second time)
-  uint8_t* zpin[2] = {nullptr, nullptr};
-  const bool zc = ncrc == 0 && zero_copy_on() && host_device_ptr(c->host[0].pin, &zpin[0]) &&
-                  host_device_ptr(c->host[1].pin, &zpin[1]);
+  uint8_t* const zpin[2] = {c->host[0].pin_dev, c->host[1].pin_dev};
+  const bool zc = ncrc == 0 && zero_copy_on() && zpin[0] && zpin[1];
   hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
@@ -224,11 +225,13 @@ hrs_status async_slot(hrs_codec* c, hrs_codec::AsyncSlot& a, size_t bytes) {
   if (a.pin) (void)hipHostFree(a.pin);
   a.dev = nullptr;
   a.pin = nullptr;
+  a.pin_dev = nullptr;
   a.bytes = 0;
   hipError_t e = hipMalloc(&a.dev, bytes);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   e = hipHostMalloc(&a.pin, bytes, hipHostMallocDefault);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  if (!host_device_ptr(a.pin, &a.pin_dev)) a.pin_dev = nullptr;
   a.bytes = bytes;
   return HRS_OK;
 }
@@ -255,8 +258,8 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
   for (int i = 0; i < nin; ++i)
     if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len});
   hrs::CopyPool::instance().run(jobs);
-  uint8_t* zpin = nullptr;  // zero copy, as host_apply_impl
-  const bool zc = ncrc == 0 && zero_copy_on() && host_device_ptr(a.pin, &zpin);
+  uint8_t* const zpin = a.pin_dev;  // zero copy, as host_apply_impl
+  const bool zc = ncrc == 0 && zero_copy_on() && zpin;
   hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
   if (nlive > 0 && !zc) {
     hipError_t e = hipMemcpyAsync(a.dev, a.pin, pitch * (nlive - 1) + len, hipMemcpyHostToDevice, a.stream);

@@ -20,6 +20,18 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine"])
+def transfer_mode(request, monkeypatch):
+    """Every test runs both ways the asynchronous rounds can move bytes: zero copy (the
+    default: kernels read and write pinned host memory across the link) and
+    the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
+    if request.param == "copy_engine":
+        monkeypatch.setenv("HRS_ZEROCOPY", "0")
+    else:
+        monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    return request.param
+
+
 def _decoder_sets(k, p, erased):
     n = k + p
     tr = C.locations_to_read(k, p, erased)

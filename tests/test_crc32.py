@@ -94,8 +94,8 @@ def test_fold_table_shared_by_slot_streams_survives_eviction(cuda):
     """two asynchronous checksummed encodes of the same row length
     run their folds on two different slot streams with one fold table; 64
     device CRC calls of other lengths then evict that table while both may
-    still be queued. Uses of a table are chained (each fold waits for the
-    previous one), so the eviction waits for both folds. Every CRC vs zlib."""
+    still be queued. Each table keeps the latest use on every stream that
+    read it, so the eviction waits for both folds. Every CRC vs zlib."""
     torch = cuda
     k, p, L = 10, 4, (256 << 10) + 40
     code = HipReedSolomonCode(k, p)

@@ -11,6 +11,18 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine"])
+def transfer_mode(request, monkeypatch):
+    """Every test runs both ways the synchronous calls can move bytes: zero copy (the
+    default: kernels read and write pinned host memory across the link) and
+    the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
+    if request.param == "copy_engine":
+        monkeypatch.setenv("HRS_ZEROCOPY", "0")
+    else:
+        monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("L", [(3 << 20) + 777, (2 << 20), 4096 + 5, 1])
 def test_host_encode_decode_multi_chunk(cuda, L):
     k, p = 10, 4

@@ -5,7 +5,7 @@ A/B, interleaved rep by rep in one process:
   zc       zero copy: the kernels read and write the pinned host memory itself
            (pinned callers: one launch over the caller's stripes; pageable:
            over the slots' pinned staging), default
-  zc_bN    zc with the grid capped at N blocks (HRS_ZC_BLOCKS=N)
+  zc_bN    zc with the grid capped at N blocks (HRS_ZC_BLOCKS=N; default 64)
 Workload = BASELINE configs[4] per GPU: RS(12,4), 256 KiB cells, 512 stripes,
 a seeded random lost pair per stripe; pinned and pageable host memory.
 
@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stripes", type=int, default=512)
-    ap.add_argument("--zc-blocks", type=int, nargs="*", default=[512, 256, 128, 64])
+    ap.add_argument("--zc-blocks", type=int, nargs="*", default=[128, 32, 16])
     args = ap.parse_args()
     k, p, L, S = 12, 4, 256 << 10, args.stripes
     n = k + p
@@ -61,7 +61,8 @@ def main():
         "encode_pinned": lambda: device.encode_batch_host(code, stn),
         "encode_pageable": lambda: device.encode_batch_host(code, pge),
     }
-    modes = {"ring": {"HRS_ZEROCOPY": "0"}, "duplex": {"HRS_ZEROCOPY": "0", "HRS_HBATCH_DUPLEX": "1"}, "zc": {}}
+    modes = {"ring": {"HRS_ZEROCOPY": "0"}, "duplex": {"HRS_ZEROCOPY": "0", "HRS_HBATCH_DUPLEX": "1"},
+             "zc": {}, "zc_uncapped": {"HRS_ZC_BLOCKS": "0"}}
     for b in args.zc_blocks:
         modes[f"zc_b{b}"] = {"HRS_ZC_BLOCKS": str(b)}
     res = {m: {leg: [] for leg in legs} for m in modes}
