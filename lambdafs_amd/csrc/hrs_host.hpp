@@ -7,9 +7,11 @@
 // Several codec handles may call concurrently (one codec per mapper / repair
 // thread: Encoder.java:80, Decoder.java:90, MapReduceBlockRepairManager.java:426),
 // so run() never serializes callers: each call posts its pieces as a batch,
-// copies its own pieces on the calling thread, and the shared workers take
-// pieces from every open batch in turn. A call returns once all its pieces
-// are copied and no worker still holds its batch.
+// copies its own pieces on the calling thread, and the shared workers join
+// the open batches in turn, each taking pieces of the batch it joined until
+// none is left (a piece per lock round trip cost a 5 MiB copy-in 40-80 us on
+// the MI355X hosts whatever the worker count: tools/pool_probe.cpp). A call
+// returns once all its pieces are copied and no worker still holds its batch.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -158,11 +160,7 @@ class CopyPool {
         }
         ++b->users;
       }
-      const size_t i = b->next.fetch_add(1);
-      if (i < b->pieces.size()) {
-        std::memcpy(b->pieces[i].dst, b->pieces[i].src, b->pieces[i].bytes);
-        b->done.fetch_add(1);
-      }
+      drain(*b);  // every piece left; one lock round trip per batch, not per piece
       {
         std::lock_guard<std::mutex> lk(mu_);
         --b->users;
