@@ -19,7 +19,8 @@ API_SRC  := hrs_api hrs_matrix hrs_dispatch hrs_hostpath hrs_batch_api
 API_OBJ  := $(patsubst %,build/%.o,$(API_SRC))
 
 JNI      := lambdafs_amd/libhrs_jni.so
-HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables
+HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
+            tests/cpp/copy_pool_test
 
 all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS)
 
@@ -96,6 +97,10 @@ tests/cpp/host_logic: tests/cpp/host_logic.cpp include/hrs.h $(LIB) $(ORACLE)
 # hipcc only for the HIP headers hrs_crc.hpp includes).
 tests/cpp/crc_tables: tests/cpp/crc_tables.cpp lambdafs_amd/csrc/crc32.hpp lambdafs_amd/csrc/hrs_crc.hpp
 	$(HIPCC) -O2 -std=c++17 -x hip --offload-arch=$(ARCH) -o $@ $<
+
+# The host copy pool under concurrent callers (CPU only).
+tests/cpp/copy_pool_test: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
+	g++ -O2 -std=c++17 -Wall -pthread -o $@ $<
 
 tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
 	g++ -O2 -std=c++17 -Wall -o $@ $< -lz

@@ -33,6 +33,20 @@ def test_host_logic_vs_oracle():
     assert out.returncode == 0 and res["ok"], res
 
 
+@pytest.mark.parametrize("threads", [0, 1, 4, 8])
+def test_copy_pool_concurrent_callers(threads):
+    """The host copy pool (hrs_host.hpp) under 4 concurrent callers posting
+    batches of 1-14 pieces of random sizes (0 B - 1 MiB): every byte lands,
+    with 0 (caller-only), 1, 4 and 8 workers draining the batches they join."""
+    exe = os.path.join(ROOT, "tests", "cpp", "copy_pool_test")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", ROOT, "tests/cpp/copy_pool_test"])
+    env = dict(os.environ, HRS_HOST_THREADS=str(threads))
+    out = subprocess.run([exe, "4", "40"], capture_output=True, text=True, timeout=300, env=env)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and res["ok"] and res["bad_jobs"] == 0, res
+
+
 @pytest.mark.parametrize("k,p", [(10, 4), (12, 4), (6, 3), (3, 2)])
 def test_harness_host_only(k, p):
     rc, res = run("--host-only", k, p)
