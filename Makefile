@@ -116,7 +116,7 @@ SAN      := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-om
 HSAN     := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
             -Xarch_host -fno-omit-frame-pointer
 ASAN_BIN := $(ASAN_DIR)/host_logic $(ASAN_DIR)/jni_harness $(ASAN_DIR)/codec_harness
-ASAN_LOG := profiles/r03/asan
+ASAN_LOG := profiles/r04/asan
 
 ASAN_API := $(patsubst %,$(ASAN_DIR)/%.o,$(API_SRC))
 $(ASAN_API): $(ASAN_DIR)/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
@@ -154,7 +154,16 @@ asan: $(ASAN_BIN)
 	  > $(ASAN_LOG)/asan_run.log 2>&1 || { cat $(ASAN_LOG)/asan_run.log; exit 1; }
 	@cat $(ASAN_LOG)/asan_run.log
 
+# ---- make tsan: the host copy pool (hrs_host.hpp: concurrent callers,
+# spinning workers that drain the batches they join) under ThreadSanitizer.
+TSAN_LOG := profiles/r04/tsan
+tsan: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
+	@mkdir -p build/tsan $(TSAN_LOG)
+	g++ -O1 -g -std=c++17 -fsanitize=thread -pthread -o build/tsan/copy_pool_test tests/cpp/copy_pool_test.cpp
+	sh -c 'for t in 0 1 4 8; do HRS_HOST_THREADS=$$t build/tsan/copy_pool_test 4 20; done' > $(TSAN_LOG)/tsan_run.log 2>&1 || { cat $(TSAN_LOG)/tsan_run.log; exit 1; }
+	@cat $(TSAN_LOG)/tsan_run.log
+
 clean:
 	rm -rf build $(LIB) $(ORACLE) $(JNI) $(HARNESS)
 
-.PHONY: all clean asan
+.PHONY: all tsan clean asan
