@@ -220,6 +220,11 @@ unsigned zero_copy_blocks() {
   return x > 0 ? static_cast<unsigned>(x) : 0u;
 }
 
+// Zero copy is taken only where the device address IS the host address
+// (HIP's unified addressing on these systems): then any pointer into a pinned
+// allocation, base or interior, is valid in a kernel as it stands, with no
+// question of how an interior pointer's offset maps. Anything else (pageable
+// memory, another mapping) takes the copy engine.
 bool host_device_ptr(const void* p, uint8_t** dp) {
   if (!p || !is_pinned(p)) return false;
   void* d = nullptr;
@@ -227,6 +232,7 @@ bool host_device_ptr(const void* p, uint8_t** dp) {
     (void)hipGetLastError();
     return false;
   }
+  if (d != p) return false;
   *dp = static_cast<uint8_t*>(d);
   return true;
 }
