@@ -185,3 +185,29 @@ def test_decode_batch_host_per_stripe_fallback_over_32_survivors(cuda):
             for t in range(len(lost)):
                 assert np.array_equal(out[s, t], ref[t]), (pinned, s, lost)
                 assert np.array_equal(out[s, t], st[s, lost[t]]), (pinned, s, lost)
+
+
+def test_host_batches_on_interior_pinned_views(cuda):
+    """Batches handed over as views that start inside a pinned allocation
+    (a caller's buffer pool): the zero-copy launch works on the view's own
+    addresses, every stripe vs the oracle (encode) and vs the lost cells
+    (repair)."""
+    torch = cuda
+    k, p, S, L = 10, 4, 16, 64 << 10
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=0)
+    rng = np.random.default_rng(11)
+    big = torch.empty((S + 5, n, L), dtype=torch.uint8, pin_memory=True).numpy()
+    st = big[5:]  # interior view
+    st[:, p:] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    st[:, :p] = 0
+    device.encode_batch_host(code, st)
+    for s in range(S):
+        ref = C.encode_bulk(k, p, [st[s, p + c].copy() for c in range(k)])
+        assert all((st[s, r] == ref[r]).all() for r in range(p)), s
+    outbig = torch.empty((S + 3, 2, L), dtype=torch.uint8, pin_memory=True).numpy()
+    out = outbig[3:]
+    er = _patterns(random.Random(5), S, n, 2, lambda s: 2)
+    device.decode_batch_host(code, st, er, out)
+    for s in range(S):
+        assert np.array_equal(out[s], st[s, er[s]]), s
