@@ -122,3 +122,61 @@ def test_device_equals_legacy_coder(cuda, k, p, L):
             legacy = C.hops_decode_via_legacy(k, p, list(host[s]), erased, ntr)
             for t in range(len(erased)):
                 assert np.array_equal(got[s, t], legacy[t]), (erased, s, t)
+
+
+def _golden():
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "tests", "golden", "bench_digests.json")) as f:
+        return json.load(f)
+
+
+def test_golden_config2_block0_through_the_legacy_coder():
+    """The committed full-size digests (made by the hops restatement) are
+    reproduced by the legacy coder alone: config 2's parity of global stripes
+    0-255 (RS(6,3), 64 KiB cells, SURVEY 8(d) synthetic stripes), encoded by
+    RSLegacyRawEncoder's restatement."""
+    import hashlib
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import stripe_digests as SD
+    import synth
+    k, p, L = 6, 3, 64 << 10
+    d = {}
+    for g in range(256):
+        data = synth.stripe_numpy(2, g, k, L)
+        h = hashlib.sha256()
+        for r in C.legacy_rs_encode(k, p, [data[c] for c in range(k)]):
+            h.update(r.tobytes())
+        d[g] = h.digest()
+    assert SD.combine(d) == {"0": _golden()["config2"]["parity"]["0"]}
+
+
+def test_golden_config5_block0_through_the_legacy_coder():
+    """Config 5's repaired cells of global stripes 0-255 (RS(12,4), 256 KiB
+    cells, each stripe's seeded lost pair): parity from the legacy encoder,
+    then the legacy decoder reading the k survivors locationsToReadForDecode
+    picks — equal to the committed digest the hops restatement made (~20 s)."""
+    import hashlib
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import stripe_digests as SD
+    import synth
+    k, p, L = 12, 4, 256 << 10
+    n = k + p
+    d = {}
+    for g in range(256):
+        data = synth.stripe_numpy(5, g, k, L)
+        parity = C.legacy_rs_encode(k, p, [data[c] for c in range(k)])
+        hops_rows = list(parity) + [data[c] for c in range(k)]  # hops order [parity..., data...]
+        er = sorted(int(x) for x in np.random.default_rng([0x5EED0005, g]).choice(n, 2, replace=False))
+        tr = sorted(C.locations_to_read(k, p, er))
+        ntr = [x for x in range(n) if x not in tr]
+        h = hashlib.sha256()
+        for o in C.hops_decode_via_legacy(k, p, hops_rows, er, ntr):
+            h.update(o.tobytes())
+        d[g] = h.digest()
+    assert SD.combine(d) == {"0": _golden()["config5"]["repaired"]["0"]}
