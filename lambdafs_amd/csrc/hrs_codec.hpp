@@ -191,6 +191,12 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
 hrs_status apply_crc_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                           size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
                           const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw);
+// Whether encode_crc_impl / apply_crc_impl (nlive live inputs) take their
+// one-pass kernel for a job of this shape, rows 16-byte aligned: the
+// zero-copy host calls checksum through host memory only then (a two-pass CRC
+// would read the cells across the link a second time).
+bool encode_crc_one_pass(const hrs_codec* c, size_t len, size_t nstripes);
+bool apply_crc_one_pass(const hrs_codec* c, int nout, int nlive, size_t len);
 
 }  // namespace hrs::api
 #pragma GCC visibility pop

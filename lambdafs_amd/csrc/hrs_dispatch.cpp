@@ -419,6 +419,20 @@ uint32_t crc_rep_mask() {
 
 // Encode + CRC-32 of the k sources and p parities (hrs_encode_crc_dev's
 // semantics) with raw window CRCs in `raw` (crc_raw_bytes_for(len, nstripes, n)).
+bool encode_crc_one_pass(const hrs_codec* c, size_t len, size_t nstripes) {
+  if (!(c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS) || !(c->kernel_mode == 0 || c->kernel_mode == 3) ||
+      fused_subs(len, nstripes) == 0)
+    return false;
+  const int k = c->k, p = c->p;  // the shapes hrs_fused.hip instantiates (launch_encode_crc)
+  if (c->kind == HRS_CODE_NRS) return (k == 10 && p == 4) || (k == 6 && p == 3);
+  return (k == 10 && p == 4) || (k == 6 && p == 3) || (k == 3 && p == 2) || (k == 12 && p == 4);
+}
+
+bool apply_crc_one_pass(const hrs_codec* c, int nout, int nlive, size_t len) {
+  return (c->kernel_mode == 0 || c->kernel_mode == 3) && len > 0 && len % hrs::kWindowBytes == 0 && nlive >= 1 &&
+         nout >= 1 && nout <= 4 && nlive <= (nout == 4 ? 8 : 12);
+}
+
 hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
                            size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
                            hipStream_t s, uint32_t* raw) {

@@ -115,13 +115,21 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     hrs_status st = host_slot(c, i, need);
     if (st != HRS_OK) return st;
   }
-  // zero copy (no checksums): the kernel reads the chunk from the slot's
-  // pinned staging and writes its outputs there, across the host link — no
-  // H2D / D2H (checksummed calls keep the device copy: their CRC pass would
-  // read the cells across the link a second time)
+  // zero copy: the kernel reads the chunk from the slot's pinned staging and
+  // writes its outputs (and the chunk CRCs) there, across the host link — no
+  // H2D / D2H. A checksummed chunk goes this way only when its one-pass
+  // kernel takes it (a two-pass CRC would read the cells across the link a
+  // second time); other chunks take the copy engine. The raw window CRCs stay
+  // in device memory.
   uint8_t* const zpin[2] = {c->host[0].pin_dev, c->host[1].pin_dev};
-  const bool zc = ncrc == 0 && zero_copy_on() && zpin[0] && zpin[1];
-  hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
+  const bool zc_ok = zero_copy_on() && zpin[0] && zpin[1];
+  auto zc_chunk = [&](size_t lj) {
+    if (!zc_ok) return false;
+    if (crc.mode == kCrcEncode) return encode_crc_one_pass(c, lj, 1);
+    if (crc.mode == kCrcOutputs) return apply_crc_one_pass(c, nout, nlive, lj);
+    return true;
+  };
+  hrs::GridCap cap(zc_ok ? zero_copy_blocks() : 0u);
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
   size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
@@ -154,6 +162,7 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     for (int i = 0; i < nin; ++i)
       if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
     pool.run(jobs);
+    const bool zc = zc_chunk(lj);
     if (nlive > 0 && !zc) {
       hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
       if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
@@ -161,7 +170,7 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     uint8_t* img = zc ? zpin[sl] : h.dev;
     for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
     for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
-    uint32_t* dcrc = reinterpret_cast<uint32_t*>(h.dev + crc_off);
+    uint32_t* dcrc = reinterpret_cast<uint32_t*>(img + crc_off);
     uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
     if (crc.mode == kCrcEncode)
       st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
@@ -259,7 +268,10 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
     if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len});
   hrs::CopyPool::instance().run(jobs);
   uint8_t* const zpin = a.pin_dev;  // zero copy, as host_apply_impl
-  const bool zc = ncrc == 0 && zero_copy_on() && zpin;
+  const bool zc = zero_copy_on() && zpin &&
+                  (crc_mode == kCrcEncode  ? encode_crc_one_pass(c, len, 1)
+                   : crc_mode == kCrcOutputs ? apply_crc_one_pass(c, nout, nlive, len)
+                                             : true);
   hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
   if (nlive > 0 && !zc) {
     hipError_t e = hipMemcpyAsync(a.dev, a.pin, pitch * (nlive - 1) + len, hipMemcpyHostToDevice, a.stream);
@@ -270,7 +282,7 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
   uint8_t* img = zc ? zpin : a.dev;
   for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
   for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
-  uint32_t* dcrc = reinterpret_cast<uint32_t*>(a.dev + crc_off);
+  uint32_t* dcrc = reinterpret_cast<uint32_t*>(img + crc_off);
   uint32_t* draw = reinterpret_cast<uint32_t*>(a.dev + raw_off);
   if (crc_mode == kCrcEncode)
     st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, a.stream, draw);

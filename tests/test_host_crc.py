@@ -24,11 +24,25 @@ def test_host_crc_exported():
     assert hasattr(L, "hrs_encode_crc") and hasattr(L, "hrs_decode_crc")
 
 
+@pytest.fixture(params=["zero_copy", "copy_engine"])
+def transfer_mode(request, monkeypatch):
+    """The GPU tests run both ways the checksummed host-buffer calls can move
+    bytes: zero copy (the default where the one-pass kernel takes the chunk:
+    kernels read and write the pinned staging, CRCs included) and the copy
+    engine (HRS_ZEROCOPY=0)."""
+    if request.param == "copy_engine":
+        monkeypatch.setenv("HRS_ZEROCOPY", "0")
+    else:
+        monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    return request.param
+
+
 def _zcrc(rows, start=None):
     return [zlib.crc32(r.tobytes(), 0 if start is None else start[i]) for i, r in enumerate(rows)]
 
 
 @pytest.mark.gpu
+@pytest.mark.usefixtures("transfer_mode")
 @pytest.mark.parametrize("L", [1 << 20, (1 << 20) + 777, (2 << 20) + (32 << 10), 4096 + 5, 1])
 def test_encode_crc_host_rs104(cuda, L):
     k, p = 10, 4
@@ -43,6 +57,7 @@ def test_encode_crc_host_rs104(cuda, L):
 
 
 @pytest.mark.gpu
+@pytest.mark.usefixtures("transfer_mode")
 def test_encode_crc_host_chained_block(cuda):
     """A block encoded cell by cell: the running CRCs after the last call
     equal the CRC32 of each whole block (CRC32.update chaining)."""
@@ -65,6 +80,7 @@ def test_encode_crc_host_chained_block(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.usefixtures("transfer_mode")
 @pytest.mark.parametrize("make", [lambda: HipNativeReedSolomonCode(10, 4), lambda: HipXORCode(10, 1),
                                   lambda: HipReedSolomonCode(12, 4, zero_inputs_after_encode=False)])
 def test_encode_crc_host_codes(cuda, make):
@@ -83,6 +99,7 @@ def test_encode_crc_host_codes(cuda, make):
 
 
 @pytest.mark.gpu
+@pytest.mark.usefixtures("transfer_mode")
 @pytest.mark.parametrize("L,erased", [((1 << 20) + 11, [4]), (256 << 10, [0, 13]), (3 << 20, [2, 5, 7, 11])])
 def test_decode_crc_host(cuda, L, erased):
     k, p = 10, 4
@@ -104,6 +121,7 @@ def test_decode_crc_host(cuda, L, erased):
 
 
 @pytest.mark.gpu
+@pytest.mark.usefixtures("transfer_mode")
 def test_crc_host_empty_rows(cuda):
     code = HipReedSolomonCode(3, 2, zero_inputs_after_encode=False)
     data = [np.zeros(0, np.uint8) for _ in range(3)]
