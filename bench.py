@@ -200,6 +200,60 @@ def cpu_baseline(k, p, L, nstripes, threads=None):
     }
 
 
+def host_calls(local, calls=100):
+    """The drop-in's synchronous call rate:
+    one RS(10,4) stripe of 1 MiB pageable rows per call through the C ABI the
+    JNI shim calls (hrs_encode / hrs_decode / hrs_encode_crc / hrs_decode_crc,
+    the Encoder.java:442 / Decoder.java:352 shapes), argument arrays built
+    once so the loop times the engine, not Python. Data shard 0 lost for the
+    decodes; the repaired row is checked."""
+    import ctypes
+    from lambdafs_amd import _lib
+    from lambdafs_amd._lib import int_array, ptr_array
+    k, p, L = 10, 4, 1 << 20
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=local, zero_inputs_after_encode=False)
+    rng = np.random.default_rng(0x5EED000A)
+    rows = [np.zeros(L, np.uint8) for _ in range(p)] + [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    h = code._handle()
+    lib = _lib.lib()
+    ins, outs = ptr_array([r.ctypes.data for r in rows[p:]]), ptr_array([r.ctypes.data for r in rows[:p]])
+    lost = np.zeros(L, np.uint8)
+    erased = [p]
+    to_read = sorted(code.locationsToReadForDecode(erased))
+    ntr = [x for x in range(n) if x not in to_read]
+    reads = ptr_array([rows[i].ctypes.data if i in to_read else None for i in range(n)])
+    lostp = ptr_array([lost.ctypes.data])
+    e_a, t_a, n_a = int_array(erased), int_array(to_read), int_array(ntr)
+    crc = (ctypes.c_uint32 * n)()
+    dcrc = (ctypes.c_uint32 * 1)()
+
+    def per_call(fn):
+        for _ in range(5):
+            code._check(fn())
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            code._check(fn())
+        return (time.perf_counter() - t0) * 1e3 / calls
+
+    res = {"what": "synchronous host-buffer calls through the C ABI (the JNI shim's calls), RS(10,4), one stripe of "
+                   "1 MiB pageable rows per call", "calls": calls}
+    res["encodeBulk_ms"] = per_call(lambda: lib.hrs_encode(h, ins, outs, L))
+    res["decodeBulk_ms"] = per_call(lambda: lib.hrs_decode(h, reads, lostp, e_a, 1, t_a, k, n_a, len(ntr), L))
+    ok = bool(np.array_equal(lost, rows[p]))
+    res["encodeBulkCrc_ms"] = per_call(lambda: lib.hrs_encode_crc(h, ins, outs, L, None, crc))
+    res["decodeBulkCrc_ms"] = per_call(lambda: lib.hrs_decode_crc(h, reads, lostp, e_a, 1, t_a, k, n_a, len(ntr), L,
+                                                                 None, dcrc))
+    ok &= bool(np.array_equal(lost, rows[p]))
+    for key in ("encodeBulk", "decodeBulk", "encodeBulkCrc", "decodeBulkCrc"):
+        res[key + "_ms"] = round(res[key + "_ms"], 4)
+        res[key + "_GiBps_user"] = round(k * L / GiB / (res[key + "_ms"] * 1e-3), 2)
+    res["bit_exact"] = ok
+    if not ok:
+        raise RuntimeError("host-buffer decode did not reproduce the lost row")
+    return res
+
+
 def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     """BASELINE configs[4] end to end through the product's host batch API
     (hrs_decode_batch_host): RS(12,4), 256 KiB cells, S stripes per GPU (4,096
@@ -845,6 +899,7 @@ def run(args):
             "e2e_config5": e2e,
             "cpu_baseline": None,
         }
+        res["host_calls"] = host_calls(local)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
             res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 40, threads=1)
