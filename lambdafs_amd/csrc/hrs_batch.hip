@@ -29,19 +29,19 @@ typedef const __attribute__((address_space(4))) int32_t* ConstIntPtr;
 template <int NOUT, int NINB, bool PATV>
 __global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const BatchArgs a) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const ConstPlanPtr plans = (ConstPlanPtr)a.plans;
   const ConstIntPtr pat = (ConstIntPtr)a.pat;
   int patv = 0;
   uint32_t k = 0;
-  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves, ++k) {
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step, ++k) {
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     int pidx;
     if constexpr (PATV) {
       if ((k & 63u) == 0) {
-        const uint64_t tl = t + static_cast<uint64_t>(lane) * nwaves;
-        patv = tl < a.ntasks ? a.pat[tl / a.nwin] : 0;
+        const uint64_t tl = t + static_cast<uint64_t>(lane) * wt.step;
+        patv = tl < wt.end ? a.pat[tl / a.nwin] : 0;
       }
       pidx = __builtin_amdgcn_readlane(patv, static_cast<int>(k & 63u));
     } else {
@@ -100,16 +100,16 @@ __device__ __forceinline__ void batch_acc_group(const ConstPlanPtr pl, int r0, i
 template <int NOUT, int D>
 __global__ void __launch_bounds__(kBlockThreads) batch_stream_kernel(const BatchArgs a) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const ConstPlanPtr plans = (ConstPlanPtr)a.plans;
   int patv = 0;
   uint32_t k = 0;
-  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves, ++k) {
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step, ++k) {
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     if ((k & 63u) == 0) {  // pattern indices of the next 64 tasks, one vector load
-      const uint64_t tl = t + static_cast<uint64_t>(lane) * nwaves;
-      patv = tl < a.ntasks ? a.pat[tl / a.nwin] : 0;
+      const uint64_t tl = t + static_cast<uint64_t>(lane) * wt.step;
+      patv = tl < wt.end ? a.pat[tl / a.nwin] : 0;
     }
     const ConstPlanPtr pl = plans + __builtin_amdgcn_readlane(patv, static_cast<int>(k & 63u));
     int nin = pl->nin;
@@ -192,7 +192,7 @@ hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
   auto kern = use_pat_prefetch() ? batch_bitsliced_kernel<NOUT, NINB, true> : batch_bitsliced_kernel<NOUT, NINB, false>;
   note_kernel_t("batch_bitsliced_kernel", NOUT, NINB, use_pat_prefetch());
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
   return hipGetLastError();
 }
 
@@ -201,7 +201,7 @@ hipError_t launch_batch_stream_n(const BatchArgs& a, hipStream_t s) {
   auto kern = batch_stream_kernel<NOUT, 4>;
   note_kernel_t("batch_stream_kernel", NOUT, 4);
   const int per_cu = NOUT >= 4 ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
   return hipGetLastError();
 }
 

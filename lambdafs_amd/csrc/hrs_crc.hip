@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include "hrs_device.hpp"
+#include "hrs_launch.hpp"
 
 namespace hrs {
 namespace {
@@ -44,8 +45,8 @@ __global__ void __launch_bounds__(kCrcBlockThreads) crc_window_kernel(const CrcW
   const uint32_t* tree = zchunk + 1024;
   const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
   const uint64_t ntasks = a.nstripes * a.nrows * wpr;
-  const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nwaves) {
+  const WaveTasks wt = wave_tasks(ntasks, a.order);
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
     const uint64_t sr = t / wpr;
     const uint64_t w = t - sr * wpr;
     const uint64_t stripe = sr / a.nrows;
@@ -152,7 +153,7 @@ hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStr
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kCrcBlockThreads), shm, s, a);
+  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kCrcBlockThreads), shm, s, with_order(a));
   return hipGetLastError();
 }
 

@@ -45,7 +45,7 @@ struct CrcWinArgs {
   int nrows;        // rows in this launch
   int row0;         // index of rows[0] among all rows of the call
   int nrows_total;  // rows of the call (raw layout [stripe][row][window])
-  int pad_;
+  int order;        // window -> wave order (task_order), set at launch
   uint64_t stride[kCrcMaxRows];  // bytes between stripes, per row
   uint64_t len;
   uint64_t nwin;    // full windows per row
@@ -88,6 +88,8 @@ struct EncodeCrcArgs {
   uint64_t nstripes;
   uint32_t subs;      // 2 KiB sub-windows per window: 1, 2, 4, 8 or 16
   uint32_t rep_mask;  // slicing-table copy of lane l = l & rep_mask (kCrcRep - 1; HRS_CRC_REP A/B)
+  int order;          // window -> wave order (task_order), set at launch
+  int pad_;
   uint32_t* raw;
   const uint32_t* tables;  // kCrcLdsWordsA words (device)
 };

@@ -103,27 +103,27 @@ __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const D
   const SliceTab slices = slice_tab(lane);
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
-  const uint32_t nwaves = gridDim.x * (kDecCrcThreads / 64);
   int nin = a.nin;
   asm volatile("" : "+s"(nin));
-  uint64_t t = wave_id_in_grid();
-  if (t >= a.ntasks) return;
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  uint64_t t = wt.t;
+  if (t >= wt.end) return;
   uint32_t ra[NINB][8], rb[NINB][8];
   uint32_t acc[NOUT][8];
   dc_load_task<NOUT, NINB>(a, t, nin, lane, ra);
-  uint64_t t1 = t + nwaves;
-  if (t1 < a.ntasks) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
-  for (;;) {  // ra: task t, rb: task t1 in flight; every wave leaves once a task index passes ntasks
+  uint64_t t1 = t + wt.step;
+  if (t1 < wt.end) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
+  for (;;) {  // ra: task t, rb: task t1 in flight; every wave leaves once a task index passes its end
     dc_apply_task<NOUT, NINB>(a, t, nin, lane, ra, acc);
-    const uint64_t t2 = t1 + nwaves;
-    if (t2 < a.ntasks) dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
+    const uint64_t t2 = t1 + wt.step;
+    if (t2 < wt.end) dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
     dc_crc_task<NOUT, DPP>(d, t, lane, slices, zchunk, tree, acc);
-    if (t1 >= a.ntasks) break;
+    if (t1 >= wt.end) break;
     dc_apply_task<NOUT, NINB>(a, t1, nin, lane, rb, acc);
-    const uint64_t t3 = t2 + nwaves;
-    if (t3 < a.ntasks) dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
+    const uint64_t t3 = t2 + wt.step;
+    if (t3 < wt.end) dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
     dc_crc_task<NOUT, DPP>(d, t1, lane, slices, zchunk, tree, acc);
-    if (t2 >= a.ntasks) break;
+    if (t2 >= wt.end) break;
     t = t2;
     t1 = t3;
   }
@@ -154,8 +154,8 @@ __global__ void __launch_bounds__(THREADS) decode_crc_kernel(const DecodeCrcArgs
   const SliceTab slices = slice_tab(lane);
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
-  const uint32_t nwaves = gridDim.x * (THREADS / 64);
-  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
     int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
     asm volatile("" : "+s"(nin));
     // written out, not through dc_load_task / dc_apply_task: with the helpers
@@ -198,6 +198,8 @@ int dcrc_threads() {
 
 template <int NOUT, int NINB>
 hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
+  DecodeCrcArgs dc = d;
+  dc.r.order = task_order();
   if constexpr (NOUT >= 2) {
     const int threads = dcrc_threads();
     auto kern = threads == 768 ? decode_crc_kernel<NOUT, NINB, 768> : decode_crc_kernel<NOUT, NINB, 512>;
@@ -210,7 +212,7 @@ hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
     uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
     if (g > static_cast<uint64_t>(cus)) g = cus;
     if (g == 0) g = 1;
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, d);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, dc);
     return hipGetLastError();
   } else {
     auto kern = dcrc_dpp() ? decode_crc_pipe_kernel<NOUT, NINB, true> : decode_crc_pipe_kernel<NOUT, NINB, false>;
@@ -223,7 +225,7 @@ hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
     uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
     if (g > static_cast<uint64_t>(cus)) g = cus;
     if (g == 0) g = 1;
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(kDecCrcThreads), shm, s, d);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(kDecCrcThreads), shm, s, dc);
     return hipGetLastError();
   }
 }

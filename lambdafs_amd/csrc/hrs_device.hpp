@@ -125,6 +125,29 @@ __device__ __forceinline__ uint32_t wave_id_in_grid() {
   return __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
 }
 
+// The tasks (2 KiB windows, task t = stripe * nwin + window) the calling wave
+// runs: t, t + step, ... below end. order 1 (the default, hrs_launch.hpp
+// task_order): block b owns the b-th of gridDim equal runs of consecutive
+// tasks and its waves take them interleaved, so each block streams one
+// contiguous region of every row; order 0: wave w of W takes w, w + W, ...
+// (grid-stride, rounds 1-4). The block range is the fastest 1:1 copy schedule
+// on this pool (tools/copy_lab.hip) and runs encode_static_kernel<10,4> on
+// bench.py's workload in 2.46 ms against 2.62 grid-stride, bit-identical
+// (tools/sched_lab.hip, profiles/r04/o/). Wave-uniform (SGPRs).
+struct WaveTasks {
+  uint64_t t, end, step;
+};
+
+__device__ __forceinline__ WaveTasks wave_tasks(uint64_t ntasks, int order) {
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (order == 0)
+    return {static_cast<uint64_t>(blockIdx.x) * wpb + w, ntasks, static_cast<uint64_t>(gridDim.x) * wpb};
+  const uint64_t per = (ntasks + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = per * blockIdx.x;
+  return {lo + w, lo + per < ntasks ? lo + per : ntasks, wpb};
+}
+
 // mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of
 // parity row o (gf::row_mask of G[o][r]). Evaluated by the compiler.
 // MATRIX is gf::EncodeMatrix<K,P> (hops RS) or gf::CauchyMatrix<K,P> (nrs).

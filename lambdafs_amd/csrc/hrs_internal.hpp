@@ -35,7 +35,7 @@ struct RowArgs {
   int nin;
   int nout;
   int accumulate;                 // 1: XOR into existing outputs (input chunking)
-  int pad_;
+  int order;                      // window -> wave order (hrs_launch.hpp task_order), set at launch
 };
 
 inline void set_coef(RowArgs& a, int o, int i, uint8_t v) {
@@ -88,6 +88,8 @@ struct BatchArgs {
   uint64_t ntasks;            // vector: nstripes * nwin; bytewise: nstripes * (len - col0)
   const BatchPlan* plans;     // device table
   const int32_t* pat;         // device: pattern index of each stripe
+  int order;                  // window -> wave order (task_order), set at launch
+  int pad_;
 };
 
 hipError_t launch_batch_bitsliced(const BatchArgs& a, int max_nout, int max_nin, hipStream_t s);

@@ -43,6 +43,20 @@ inline int device_cus() {
   return cus;
 }
 
+// Window -> wave order of the streaming kernels (hrs_device.hpp wave_tasks):
+// 1 = block range (default), 0 = grid-stride. HRS_TASK_ORDER=0 selects the
+// old order; read per launch, so one process can A/B both (tools/bench_order.py).
+inline int task_order() {
+  const char* e = getenv("HRS_TASK_ORDER");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
+template <class A>
+inline A with_order(A a) {
+  a.order = task_order();
+  return a;
+}
+
 // Streaming kernels: a fixed number of resident blocks per CU, grid-striding
 // over the tasks. 2 x 256-thread blocks per CU (8 waves, each with a whole
 // window's rows in flight) measured fastest for both the static and the

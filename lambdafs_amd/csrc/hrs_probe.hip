@@ -10,7 +10,8 @@
 //     (hrs_probe_rows): 2 KiB column windows of `nread` rows of a stripe-major
 //     [S][nrows][L] buffer read, `nwrite` rows written, nontemporal 16-byte
 //     accesses, one wave task per window, as encode_static_kernel and the
-//     pipelined repair kernel walk them, under a few load schedules.
+//     pipelined repair kernel walk them (same window order, HRS_TASK_ORDER),
+//     under a few load schedules.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -121,12 +122,12 @@ __device__ __forceinline__ u32x4 pace_work(u32x4 x) {
 
 template <int R, int W, int D, int M>
 __global__ void __launch_bounds__(256) rows_kernel(uint8_t* __restrict__ base, uint64_t nstripes, int nrows,
-                                                    uint64_t L) {
+                                                    uint64_t L, int order) {
   const int lane = threadIdx.x & 63;
   const uint64_t nwin = L / 2048u;
   const uint64_t ntasks = nstripes * nwin;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
-  for (uint64_t t = wave_id_in_grid(); t < ntasks; t += nw) {
+  const WaveTasks wt = wave_tasks(ntasks, order);  // the coding kernels' window order
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
     const uint64_t s = t / nwin;
     uint8_t* sb = base + s * nrows * L + (t - s * nwin) * 2048u + lane * 16;
     u32x4 v[R][2];
@@ -196,7 +197,7 @@ template <int R, int W, int D, int M>
 hrs_status launch_rows_dm(void* base, size_t nstripes, int nrows, size_t L, unsigned grid, hipStream_t st) {
   auto k = rows_kernel<R, W, D, M>;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<uint8_t*>(base), static_cast<uint64_t>(nstripes),
-                     nrows, static_cast<uint64_t>(L));
+                     nrows, static_cast<uint64_t>(L), task_order());
   return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
 }
 

@@ -16,8 +16,8 @@ namespace {
 template <int NOUT, int NINB>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
     int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
     asm volatile("" : "+s"(nin));
     const uint64_t stripe = t / a.nwin;
@@ -101,22 +101,22 @@ template <int NOUT, int NINB>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_pipe_kernel(const RowArgs a) {
   static_assert(!BitLoop<NOUT, NINB>::kRolled, "pipelined kernel takes the unrolled shapes only");
   const int lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   int nin = a.nin;
   asm volatile("" : "+s"(nin));
-  uint64_t t = wave_id_in_grid();
-  if (t >= a.ntasks) return;
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  uint64_t t = wt.t;
+  if (t >= wt.end) return;
   uint32_t ra[NINB][8], rb[NINB][8];
   load_task<NOUT, NINB>(a, t, nin, lane, ra);
-  for (;;) {  // every wave leaves once its next task index passes ntasks
-    const uint64_t t1 = t + nwaves;
-    if (t1 < a.ntasks) load_task<NOUT, NINB>(a, t1, nin, lane, rb);
+  for (;;) {  // every wave leaves once its next task index passes its end
+    const uint64_t t1 = t + wt.step;
+    if (t1 < wt.end) load_task<NOUT, NINB>(a, t1, nin, lane, rb);
     apply_task<NOUT, NINB>(a, t, nin, lane, ra);
-    if (t1 >= a.ntasks) break;
-    const uint64_t t2 = t1 + nwaves;
-    if (t2 < a.ntasks) load_task<NOUT, NINB>(a, t2, nin, lane, ra);
+    if (t1 >= wt.end) break;
+    const uint64_t t2 = t1 + wt.step;
+    if (t2 < wt.end) load_task<NOUT, NINB>(a, t2, nin, lane, ra);
     apply_task<NOUT, NINB>(a, t1, nin, lane, rb);
-    if (t2 >= a.ntasks) break;
+    if (t2 >= wt.end) break;
     t = t2;
   }
 }
@@ -151,8 +151,8 @@ __device__ __forceinline__ void acc_group(const RowArgs& a, int r0, int nin, uin
 template <int NOUT, int D>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_stream_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  for (uint64_t t = wave_id_in_grid(); t < a.ntasks; t += nwaves) {
+  const WaveTasks wt = wave_tasks(a.ntasks, a.order);
+  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
     int nin = a.nin;
     asm volatile("" : "+s"(nin));
     const uint64_t stripe = t / a.nwin;
@@ -220,7 +220,7 @@ hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
     }
   note_kernel_t(name, NOUT, NINB);
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
   return hipGetLastError();
 }
 
@@ -240,7 +240,7 @@ hipError_t launch_stream_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_stream_kernel<NOUT, kStreamGroup>;
   note_kernel_t("bitsliced_stream_kernel", NOUT, kStreamGroup);
   const int per_cu = NOUT >= 4 ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
   return hipGetLastError();
 }
 
