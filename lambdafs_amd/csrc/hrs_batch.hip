@@ -34,13 +34,15 @@ __global__ void __launch_bounds__(kBlockThreads) batch_bitsliced_kernel(const Ba
   int patv = 0;
   uint32_t k = 0;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step, ++k) {
+  for (;; ++k) {
+    const uint64_t t = wt.at(k);
+    if (t >= wt.end) break;
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     int pidx;
     if constexpr (PATV) {
       if ((k & 63u) == 0) {
-        const uint64_t tl = t + static_cast<uint64_t>(lane) * wt.step;
+        const uint64_t tl = wt.at(k + static_cast<uint32_t>(lane));
         patv = tl < wt.end ? a.pat[tl / a.nwin] : 0;
       }
       pidx = __builtin_amdgcn_readlane(patv, static_cast<int>(k & 63u));
@@ -104,11 +106,13 @@ __global__ void __launch_bounds__(kBlockThreads) batch_stream_kernel(const Batch
   int patv = 0;
   uint32_t k = 0;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step, ++k) {
+  for (;; ++k) {
+    const uint64_t t = wt.at(k);
+    if (t >= wt.end) break;
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     if ((k & 63u) == 0) {  // pattern indices of the next 64 tasks, one vector load
-      const uint64_t tl = t + static_cast<uint64_t>(lane) * wt.step;
+      const uint64_t tl = wt.at(k + static_cast<uint32_t>(lane));
       patv = tl < wt.end ? a.pat[tl / a.nwin] : 0;
     }
     const ConstPlanPtr pl = plans + __builtin_amdgcn_readlane(patv, static_cast<int>(k & 63u));
@@ -192,7 +196,7 @@ hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
   auto kern = use_pat_prefetch() ? batch_bitsliced_kernel<NOUT, NINB, true> : batch_bitsliced_kernel<NOUT, NINB, false>;
   note_kernel_t("batch_bitsliced_kernel", NOUT, NINB, use_pat_prefetch());
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderBatch));
   return hipGetLastError();
 }
 
@@ -201,7 +205,7 @@ hipError_t launch_batch_stream_n(const BatchArgs& a, hipStream_t s) {
   auto kern = batch_stream_kernel<NOUT, 4>;
   note_kernel_t("batch_stream_kernel", NOUT, 4);
   const int per_cu = NOUT >= 4 ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderBatch));
   return hipGetLastError();
 }
 

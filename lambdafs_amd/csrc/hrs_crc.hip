@@ -46,7 +46,9 @@ __global__ void __launch_bounds__(kCrcBlockThreads) crc_window_kernel(const CrcW
   const uint64_t wpr = a.nwin + (a.tail ? 1 : 0);
   const uint64_t ntasks = a.nstripes * a.nrows * wpr;
   const WaveTasks wt = wave_tasks(ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     const uint64_t sr = t / wpr;
     const uint64_t w = t - sr * wpr;
     const uint64_t stripe = sr / a.nrows;
@@ -153,7 +155,7 @@ hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStr
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kCrcBlockThreads), shm, s, with_order(a));
+  hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kCrcBlockThreads), shm, s, with_order(a, kOrderCrc));
   return hipGetLastError();
 }
 

@@ -106,21 +106,22 @@ __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const D
   int nin = a.nin;
   asm volatile("" : "+s"(nin));
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  uint64_t t = wt.t;
+  uint32_t j = 0;
+  uint64_t t = wt.at(0);
   if (t >= wt.end) return;
   uint32_t ra[NINB][8], rb[NINB][8];
   uint32_t acc[NOUT][8];
   dc_load_task<NOUT, NINB>(a, t, nin, lane, ra);
-  uint64_t t1 = t + wt.step;
+  uint64_t t1 = wt.at(++j);
   if (t1 < wt.end) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
   for (;;) {  // ra: task t, rb: task t1 in flight; every wave leaves once a task index passes its end
     dc_apply_task<NOUT, NINB>(a, t, nin, lane, ra, acc);
-    const uint64_t t2 = t1 + wt.step;
+    const uint64_t t2 = wt.at(++j);
     if (t2 < wt.end) dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
     dc_crc_task<NOUT, DPP>(d, t, lane, slices, zchunk, tree, acc);
     if (t1 >= wt.end) break;
     dc_apply_task<NOUT, NINB>(a, t1, nin, lane, rb, acc);
-    const uint64_t t3 = t2 + wt.step;
+    const uint64_t t3 = wt.at(++j);
     if (t3 < wt.end) dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
     dc_crc_task<NOUT, DPP>(d, t1, lane, slices, zchunk, tree, acc);
     if (t2 >= wt.end) break;
@@ -155,7 +156,9 @@ __global__ void __launch_bounds__(THREADS) decode_crc_kernel(const DecodeCrcArgs
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
     asm volatile("" : "+s"(nin));
     // written out, not through dc_load_task / dc_apply_task: with the helpers
@@ -199,7 +202,7 @@ int dcrc_threads() {
 template <int NOUT, int NINB>
 hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
   DecodeCrcArgs dc = d;
-  dc.r.order = task_order();
+  dc.r.order = task_order(kOrderDecodeCrc);
   if constexpr (NOUT >= 2) {
     const int threads = dcrc_threads();
     auto kern = threads == 768 ? decode_crc_kernel<NOUT, NINB, 768> : decode_crc_kernel<NOUT, NINB, 512>;

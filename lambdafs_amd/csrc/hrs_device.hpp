@@ -126,26 +126,38 @@ __device__ __forceinline__ uint32_t wave_id_in_grid() {
 }
 
 // The tasks (2 KiB windows, task t = stripe * nwin + window) the calling wave
-// runs: t, t + step, ... below end. order 1 (the default, hrs_launch.hpp
-// task_order): block b owns the b-th of gridDim equal runs of consecutive
-// tasks and its waves take them interleaved, so each block streams one
-// contiguous region of every row; order 0: wave w of W takes w, w + W, ...
-// (grid-stride, rounds 1-4). The block range is the fastest 1:1 copy schedule
-// on this pool (tools/copy_lab.hip) and runs encode_static_kernel<10,4> on
-// bench.py's workload in 2.46 ms against 2.62 grid-stride, bit-identical
-// (tools/sched_lab.hip, profiles/r04/o/). Wave-uniform (SGPRs).
+// runs, in order: at(0), at(1), ... while below end. `order` (hrs_launch.hpp
+// task_order) picks the window -> wave assignment:
+//   C >= 1  block-cyclic: block b takes chunks b, b + G, ... of C * wpb
+//           consecutive tasks, its waves interleaved within a chunk (C = 1 is
+//           the grid-stride order of rounds 1-4: wave w of W takes w, w + W, ...);
+//   0       block range: block b owns the b-th of G equal runs of consecutive
+//           tasks (one chunk per block), so each block streams one contiguous
+//           region of every row, as the fastest 1:1 copy on this pool does
+//           (tools/copy_lab.hip).
+// Measured per kernel family (tools/sched_lab.hip, tools/bench_order.py,
+// profiles/r04/o/, p/, q/). Wave-uniform (SGPRs); at() is a few VALU/SALU ops
+// per task.
 struct WaveTasks {
-  uint64_t t, end, step;
+  uint64_t t0, end, jump;  // jump: tasks between a wave's chunks (G * C * wpb)
+  uint32_t chunk, wpb;     // tasks per wave per chunk (block range: 2^32 - 1)
+
+  __device__ __forceinline__ uint64_t at(uint32_t j) const {
+    const uint32_t q = j / chunk;
+    return t0 + q * jump + static_cast<uint64_t>(j - q * chunk) * wpb;
+  }
 };
 
 __device__ __forceinline__ WaveTasks wave_tasks(uint64_t ntasks, int order) {
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (order == 0)
-    return {static_cast<uint64_t>(blockIdx.x) * wpb + w, ntasks, static_cast<uint64_t>(gridDim.x) * wpb};
+  if (order >= 1) {
+    const uint32_t c = static_cast<uint32_t>(order);
+    return {static_cast<uint64_t>(blockIdx.x) * c * wpb + w, ntasks, static_cast<uint64_t>(gridDim.x) * c * wpb, c, wpb};
+  }
   const uint64_t per = (ntasks + gridDim.x - 1) / gridDim.x;
   const uint64_t lo = per * blockIdx.x;
-  return {lo + w, lo + per < ntasks ? lo + per : ntasks, wpb};
+  return {lo + w, lo + per < ntasks ? lo + per : ntasks, 0, 0xFFFFFFFFu, wpb};
 }
 
 // mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of

@@ -41,7 +41,9 @@ __global__ void __launch_bounds__(THREADS) encode_crc_kernel(const EncodeCrcArgs
   const uint32_t* tree = zchunk + 1024;
   const uint64_t ntasks = a.nstripes * a.nwin;
   const WaveTasks wt = wave_tasks(ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     const uint64_t stripe = t / a.nwin;
     const uint64_t w = t - stripe * a.nwin;
     const uint64_t in_base = stripe * a.in_stride + w * a.subs * kWindowBytes;
@@ -165,7 +167,9 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
   const uint32_t* tree = zchunk + 1024;
   const uint64_t ntasks = a.nstripes * a.nwin;
   const WaveTasks wt = wave_tasks(ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     const uint64_t stripe = t / a.nwin;
     const uint64_t w = t - stripe * a.nwin;
     const uint64_t in_base = stripe * a.in_stride + w * a.subs * kWindowBytes;
@@ -320,7 +324,7 @@ hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   uint64_t g = (ntasks + per_block - 1) / per_block;
   if (g > static_cast<uint64_t>(cus)) g = cus;
   if (g == 0) g = 1;
-  hipLaunchKernelGGL(k.k, dim3(static_cast<unsigned>(g)), dim3(k.threads), shm, s, with_order(a));
+  hipLaunchKernelGGL(k.k, dim3(static_cast<unsigned>(g)), dim3(k.threads), shm, s, with_order(a, kOrderFusedEncode));
   return hipGetLastError();
 }
 

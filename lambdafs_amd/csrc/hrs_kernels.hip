@@ -47,7 +47,9 @@ template <int K, int P, class MATRIX>
 __device__ __forceinline__ void encode_static_body(const RowArgs& a) {
   const int lane = threadIdx.x & 63;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     uint32_t acc[P][8];
@@ -101,7 +103,9 @@ __global__ void __launch_bounds__(kBlockThreads) xor_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const int nin = a.nin;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     const uint64_t in_base = stripe * a.in_stride + off;
@@ -170,7 +174,7 @@ hipError_t launch_static(const RowArgs& a, hipStream_t s) {
   auto kern = encode_static_kernel<K, P>;
   note_kernel_t("encode_static_kernel", K, P);
   const unsigned g = stream_grid(a.ntasks);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, with_order(a, kOrderStaticEncode));
   return hipGetLastError();
 }
 
@@ -179,7 +183,7 @@ hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
   auto kern = encode_cauchy_kernel<K, P>;
   note_kernel_t("encode_cauchy_kernel", K, P);
   const unsigned g = stream_grid(a.ntasks);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, with_order(a, kOrderStaticEncode));
   return hipGetLastError();
 }
 
@@ -213,7 +217,7 @@ template <int NINB>
 hipError_t launch_xor_n(const RowArgs& a, hipStream_t s) {
   auto kern = xor_kernel<NINB>;
   note_kernel_t("xor_kernel", NINB);
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, with_order(a, kOrderStaticEncode));
   return hipGetLastError();
 }
 

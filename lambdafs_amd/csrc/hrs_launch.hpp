@@ -43,17 +43,31 @@ inline int device_cus() {
   return cus;
 }
 
-// Window -> wave order of the streaming kernels (hrs_device.hpp wave_tasks):
-// 1 = block range (default), 0 = grid-stride. HRS_TASK_ORDER=0 selects the
-// old order; read per launch, so one process can A/B both (tools/bench_order.py).
-inline int task_order() {
+// Window -> wave order of a streaming kernel launch (hrs_device.hpp
+// wave_tasks): C >= 1 = block-cyclic chunks of C windows per wave (1 = grid-
+// stride), 0 = block range. Each kernel family passes its measured default;
+// HRS_TASK_ORDER=<C> overrides every family (A/B runs), read per launch so
+// one process can sweep it (tools/bench_order.py).
+inline int task_order(int dflt) {
   const char* e = getenv("HRS_TASK_ORDER");
-  return (e && e[0] == '0') ? 0 : 1;
+  if (e && *e) {
+    const int c = atoi(e);
+    if (c >= 0 && c <= 4096) return c;
+  }
+  return dflt;
 }
 
+// Measured defaults per family (profiles/r04/q/order_sweep.jsonl).
+constexpr int kOrderStaticEncode = 1;  // encode_static / encode_cauchy / xor
+constexpr int kOrderRuntime = 1;       // bitsliced (plain, pipelined, streaming) repairs
+constexpr int kOrderBatch = 1;         // heterogeneous repair batches
+constexpr int kOrderFusedEncode = 1;   // encode + CRC-32
+constexpr int kOrderDecodeCrc = 1;     // repair + CRC-32
+constexpr int kOrderCrc = 1;           // CRC-32 windows
+
 template <class A>
-inline A with_order(A a) {
-  a.order = task_order();
+inline A with_order(A a, int dflt) {
+  a.order = task_order(dflt);
   return a;
 }
 

@@ -127,7 +127,9 @@ __global__ void __launch_bounds__(256) rows_kernel(uint8_t* __restrict__ base, u
   const uint64_t nwin = L / 2048u;
   const uint64_t ntasks = nstripes * nwin;
   const WaveTasks wt = wave_tasks(ntasks, order);  // the coding kernels' window order
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     const uint64_t s = t / nwin;
     uint8_t* sb = base + s * nrows * L + (t - s * nwin) * 2048u + lane * 16;
     u32x4 v[R][2];
@@ -197,7 +199,7 @@ template <int R, int W, int D, int M>
 hrs_status launch_rows_dm(void* base, size_t nstripes, int nrows, size_t L, unsigned grid, hipStream_t st) {
   auto k = rows_kernel<R, W, D, M>;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, static_cast<uint8_t*>(base), static_cast<uint64_t>(nstripes),
-                     nrows, static_cast<uint64_t>(L), task_order());
+                     nrows, static_cast<uint64_t>(L), task_order(kOrderStaticEncode));
   return hipGetLastError() == hipSuccess ? HRS_OK : HRS_EDEVICE;
 }
 

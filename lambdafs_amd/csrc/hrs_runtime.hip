@@ -17,7 +17,9 @@ template <int NOUT, int NINB>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
     asm volatile("" : "+s"(nin));
     const uint64_t stripe = t / a.nwin;
@@ -104,16 +106,17 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_pipe_kernel(const Row
   int nin = a.nin;
   asm volatile("" : "+s"(nin));
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  uint64_t t = wt.t;
+  uint32_t j = 0;
+  uint64_t t = wt.at(0);
   if (t >= wt.end) return;
   uint32_t ra[NINB][8], rb[NINB][8];
   load_task<NOUT, NINB>(a, t, nin, lane, ra);
   for (;;) {  // every wave leaves once its next task index passes its end
-    const uint64_t t1 = t + wt.step;
+    const uint64_t t1 = wt.at(++j);
     if (t1 < wt.end) load_task<NOUT, NINB>(a, t1, nin, lane, rb);
     apply_task<NOUT, NINB>(a, t, nin, lane, ra);
     if (t1 >= wt.end) break;
-    const uint64_t t2 = t1 + wt.step;
+    const uint64_t t2 = wt.at(++j);
     if (t2 < wt.end) load_task<NOUT, NINB>(a, t2, nin, lane, ra);
     apply_task<NOUT, NINB>(a, t1, nin, lane, rb);
     if (t2 >= wt.end) break;
@@ -152,7 +155,9 @@ template <int NOUT, int D>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_stream_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  for (uint64_t t = wt.t; t < wt.end; t += wt.step) {
+  for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
+    const uint64_t t = wt.at(j);
+    if (t >= wt.end) break;
     int nin = a.nin;
     asm volatile("" : "+s"(nin));
     const uint64_t stripe = t / a.nwin;
@@ -220,7 +225,7 @@ hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
     }
   note_kernel_t(name, NOUT, NINB);
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderRuntime));
   return hipGetLastError();
 }
 
@@ -240,7 +245,7 @@ hipError_t launch_stream_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_stream_kernel<NOUT, kStreamGroup>;
   note_kernel_t("bitsliced_stream_kernel", NOUT, kStreamGroup);
   const int per_cu = NOUT >= 4 ? 3 : 2;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a));
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderRuntime));
   return hipGetLastError();
 }
 

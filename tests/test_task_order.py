@@ -1,7 +1,7 @@
-"""Window -> wave orders (hrs_device.hpp wave_tasks; HRS_TASK_ORDER 0 =
-grid-stride, 1 = block range, the default) against the oracle on task counts
-that do not divide evenly: fewer tasks than one block's waves, a last block
-with a short range, ranges that are not a multiple of the block's waves, and
+"""Window -> wave orders (hrs_device.hpp wave_tasks; HRS_TASK_ORDER 1 =
+grid-stride, 0 = block range, C > 1 = block-cyclic chunks of C windows per
+wave) against the oracle on task counts that do not divide evenly: fewer
+tasks than one block's waves, a last block with a short range, ranges that are not a multiple of the block's waves, and
 row tails (the byte-granular kernel) beside whole windows. Every streaming
 kernel family: static encode, fused encode + CRC, the pipelined and plain
 repairs, fused repair + CRC, the heterogeneous repair batch, CRC-32 windows.
@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(1, 2048), (3, 6144), (7, 2048 * 5 + 100), (513, 4096), (300, 65536)]
 
 
-@pytest.fixture(params=[0, 1], ids=["grid_stride", "block_range"])
+@pytest.fixture(params=[1, 0, 4, 32], ids=["grid_stride", "block_range", "cyclic4", "cyclic32"])
 def order(request, monkeypatch):
     monkeypatch.setenv("HRS_TASK_ORDER", str(request.param))
     return request.param

@@ -1,8 +1,9 @@
-"""Window -> wave order A/B (HRS_TASK_ORDER: 0 = grid-stride, rounds 1-4;
-1 = block range, hrs_device.hpp wave_tasks) over every streaming kernel the
-bench and the BASELINE configs run, in one process: the two orders alternate
-per rep (the variable is read per launch), medians of HIP-event times on the
-launch stream; every output of order 1 is compared with order 0's.
+"""Window -> wave order sweep (HRS_TASK_ORDER, hrs_device.hpp wave_tasks:
+C >= 1 = block-cyclic chunks of C windows per wave, 1 = the grid-stride order
+of rounds 1-4; 0 = block range) over every streaming kernel the bench and the
+BASELINE configs run, in one process: the orders alternate per rep (the
+variable is read per launch), medians of HIP-event times on the launch
+stream; every order's outputs are compared with order 1's.
 Workloads: bench.py's RS(10,4) 1 MiB x 1,024 (encode, fused encode + CRC,
 1-4 erasure repairs, fused repair + CRC, random-location repair batches of
 1 and 2 losses, CRC-32 of the data rows) and configs 4/5's RS(12,4)
@@ -24,7 +25,9 @@ from lambdafs_amd import HipReedSolomonCode, device  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--orders", default="1,2,4,8,16,32,0")
 args = ap.parse_args()
+ORDERS = [int(x) for x in args.orders.split(",")]
 
 
 def timed(fn):
@@ -90,33 +93,37 @@ def workloads():
 
 
 def main():
-    res = []
+    bad = []
     for name, code, fn, snap, target, nbytes in workloads():
-        times = {0: [], 1: []}
-        outs = {}
-        for o in (0, 1):
+        times = {o: [] for o in ORDERS}
+        outs, kern = {}, {}
+        for o in ORDERS:
             set_order(o)
             if target is not None:
                 target.fill_(0xA5)  # a task the order skips would leave this behind
             r = fn()
             torch.cuda.synchronize()
             outs[o] = snap(r)
-            outs[o + 10] = code.lastKernel()
+            kern[o] = code.lastKernel()
         for _ in range(args.reps):
-            for o in (0, 1):
+            for o in ORDERS:
                 set_order(o)
                 fn()
                 torch.cuda.synchronize()
                 times[o].append(timed(fn))
-        t0, t1 = float(np.median(times[0])), float(np.median(times[1]))
-        row = {"workload": name, "kernel": outs[11], "grid_stride_ms": round(t0, 4), "block_range_ms": round(t1, 4),
-               "speedup": round(t0 / t1, 4), "block_range_TBps": round(nbytes / 1e12 / (t1 * 1e-3), 3),
-               "identical": bool(torch.equal(outs[0], outs[1])), "same_kernel": outs[10] == outs[11]}
+        ms = {o: float(np.median(times[o])) for o in ORDERS}
+        best = min(ORDERS, key=lambda o: ms[o])
+        ident = {o: bool(torch.equal(outs[o], outs[ORDERS[0]])) for o in ORDERS}
+        row = {"workload": name, "kernel": kern[ORDERS[0]], "ms": {str(o): round(ms[o], 4) for o in ORDERS},
+               "best_order": best, "best_vs_grid_stride": round(ms[1] / ms[best], 4) if 1 in ms else None,
+               "best_TBps": round(nbytes / 1e12 / (ms[best] * 1e-3), 3), "identical": all(ident.values()),
+               "same_kernel": len(set(kern.values())) == 1}
         print(json.dumps(row), flush=True)
-        res.append(row)
+        if not row["identical"]:
+            bad.append(name)
         del outs
-    set_order(1)
-    assert all(r["identical"] for r in res), "order changed an output"
+    os.environ.pop("HRS_TASK_ORDER", None)
+    assert not bad, f"order changed an output: {bad}"
 
 
 if __name__ == "__main__":

@@ -199,6 +199,7 @@ int main(int argc, char** argv) {
   a.ntasks = S * a.nwin;
   a.nin = K;
   a.nout = P;
+  a.order = 1;  // the product kernel in its grid-stride order (hrs_device.hpp wave_tasks)
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
 
