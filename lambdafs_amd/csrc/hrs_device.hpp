@@ -135,14 +135,19 @@ __device__ __forceinline__ uint32_t wave_id_in_grid() {
 //           tasks (one chunk per block), so each block streams one contiguous
 //           region of every row, as the fastest 1:1 copy on this pool does
 //           (tools/copy_lab.hip).
-// Measured per kernel family (tools/sched_lab.hip, tools/bench_order.py,
-// profiles/r04/o/, p/, q/). Wave-uniform (SGPRs); at() is a few VALU/SALU ops
-// per task.
+// Measured (tools/sched_lab.hip, bench_order.py, order_shapes.py; profiles/
+// r04/o, q, r, s): no order wins across shapes and boxes. The block range ran
+// bench.py's RS(10,4) 1 MiB x 1,024 encode 3-7 % faster on four boxes and
+// 6 % slower on a fifth, and lost 5-25 % on RS(12,4) and small jobs; the
+// repairs prefer grid-stride or pairs (C = 2) by 0-3 %. Every family keeps
+// grid-stride (hrs_launch.hpp kOrder*); the other orders stay as A/B knobs.
+// Wave-uniform (SGPRs); at() is a few VALU/SALU ops per task.
 struct WaveTasks {
   uint64_t t0, end, jump;  // jump: tasks between a wave's chunks (G * C * wpb)
   uint32_t chunk, wpb;     // tasks per wave per chunk (block range: 2^32 - 1)
 
   __device__ __forceinline__ uint64_t at(uint32_t j) const {
+    if (chunk == 1) return t0 + j * jump;  // grid-stride, the default: no division
     const uint32_t q = j / chunk;
     return t0 + q * jump + static_cast<uint64_t>(j - q * chunk) * wpb;
   }

@@ -57,7 +57,8 @@ inline int task_order(int dflt) {
   return dflt;
 }
 
-// Measured defaults per family (profiles/r04/q/order_sweep.jsonl).
+// Defaults per family: grid-stride throughout (hrs_device.hpp wave_tasks,
+// profiles/r04/q/order_sweep.jsonl, r/ and s/order_shapes.jsonl).
 constexpr int kOrderStaticEncode = 1;  // encode_static / encode_cauchy / xor
 constexpr int kOrderRuntime = 1;       // bitsliced (plain, pipelined, streaming) repairs
 constexpr int kOrderBatch = 1;         // heterogeneous repair batches

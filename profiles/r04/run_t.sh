@@ -1,0 +1,9 @@
+#!/bin/bash
+# Tree after the window-order knob (grid-stride default): order parity, the
+# full GPU suite, smoke, bench.
+set -e
+O=gpurun_out/r04t
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gpu_tests.txt 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
+timeout -k 10 400 python bench.py > $O/bench.jsonl 2> $O/bench.err

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(1, 2048), (3, 6144), (7, 2048 * 5 + 100), (513, 4096), (300, 65536)]
 
 
-@pytest.fixture(params=[1, 0, 4, 32], ids=["grid_stride", "block_range", "cyclic4", "cyclic32"])
+@pytest.fixture(params=[1, 0, 2, 32], ids=["grid_stride", "block_range", "cyclic2", "cyclic32"])
 def order(request, monkeypatch):
     monkeypatch.setenv("HRS_TASK_ORDER", str(request.param))
     return request.param
