@@ -74,6 +74,9 @@ def parse(argv=None):
     ap.add_argument("--no-e2e", action="store_true", help="skip the config-5 end-to-end (host memory) leg")
     ap.add_argument("--no-sha", action="store_true", help="skip the per-rank parity SHA-256")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-calls", action="store_true",
+                    help="skip the synchronous C-ABI call leg (its small launches of the bench's kernels would mix "
+                         "into a rocprofv3 per-kernel average: profiles/run_rocprof.sh passes this)")
     ap.add_argument("--check", action="store_true", help="verify a sample against the oracle after timing")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
@@ -899,7 +902,7 @@ def run(args):
             "e2e_config5": e2e,
             "cpu_baseline": None,
         }
-        res["host_calls"] = host_calls(local)
+        res["host_calls"] = None if args.no_host_calls else host_calls(local)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
             res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 40, threads=1)

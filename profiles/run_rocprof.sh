@@ -12,10 +12,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$REPO/bench.py" --no-cpu-baseline "$@" > "$OUT/trace_bench.log" 2>&1
+  python3 "$REPO/bench.py" --no-cpu-baseline --no-host-calls "$@" > "$OUT/trace_bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-  python3 "$REPO/bench.py" --no-cpu-baseline "$@" > "$OUT/pmc_fetch_bench.log" 2>&1
+  python3 "$REPO/bench.py" --no-cpu-baseline --no-host-calls "$@" > "$OUT/pmc_fetch_bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-  python3 "$REPO/bench.py" --no-cpu-baseline "$@" > "$OUT/pmc_write_bench.log" 2>&1
+  python3 "$REPO/bench.py" --no-cpu-baseline --no-host-calls "$@" > "$OUT/pmc_write_bench.log" 2>&1
 cd /tmp && timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc_sq" -o run -- \
-  python3 "$REPO/bench.py" --no-cpu-baseline "$@" > "$OUT/pmc_sq_bench.log" 2>&1
+  python3 "$REPO/bench.py" --no-cpu-baseline --no-host-calls "$@" > "$OUT/pmc_sq_bench.log" 2>&1
