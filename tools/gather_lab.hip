@@ -237,6 +237,94 @@ __global__ void __launch_bounds__(256) phased_reg_kernel(uint8_t* __restrict__ b
   }
 }
 
+// p-structure (flush whenever the write window comes) with the buffered
+// outputs in registers: slot nb (wave-uniform) is written through a switch,
+// so every register index is static.
+template <int R, int W, int B, bool PRED = false>
+__global__ void __launch_bounds__(256) phased_sw_kernel(uint8_t* __restrict__ base, uint64_t period, uint64_t wwin,
+                                                        unsigned long long* stats = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t ntasks = kS * kNwin;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * 4;
+  const uint64_t rstart = period - wwin;
+  u4 oa[B][W], ob[B][W];
+  int nb = 0;
+  uint64_t tfirst = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      if (i >= nb) break;
+      const uint64_t t = tfirst + i * nw;
+      const uint64_t s = t / kNwin;
+      const uint64_t off = (t - s * kNwin) * 2048u + lane * 16u;
+      uint8_t* sb = base + s * kN * kL + off;
+#pragma unroll
+      for (int o = 0; o < W; ++o) {
+        u4* q = reinterpret_cast<u4*>(sb + o * kL);
+        __builtin_nontemporal_store(oa[i][o], q);
+        __builtin_nontemporal_store(ob[i][o], q + 64);
+      }
+    }
+    nb = 0;
+  };
+  uint64_t est = 0;  // PRED: the wave's recent task time (ticks)
+  uint64_t busy = 0, ntask = 0;  // stats: read-phase task time, tasks
+  for (uint64_t t = wave_gid(); t < ntasks; t += nw) {
+    const uint64_t t_start = rt();
+    uint64_t ph = t_start % period;
+    // PRED: a task that would still be loading when the write window opens
+    // is not started (its reads would mix with the other waves' writes)
+    if (nb == B || ph >= rstart || (PRED && ph + est >= rstart)) {
+      while (ph < rstart) {
+        __builtin_amdgcn_s_sleep(2);
+        ph = rt() % period;
+      }
+      flush();
+      const uint64_t p0 = rt() / period;
+      while (rt() / period == p0 && rt() % period >= rstart) __builtin_amdgcn_s_sleep(2);
+    }
+    const uint64_t t_go = rt();
+    const uint64_t s = t / kNwin;
+    const uint64_t off = (t - s * kNwin) * 2048u + lane * 16u;
+    const uint8_t* sb = base + s * kN * kL + off;
+    u4 v[R][2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u4* p = reinterpret_cast<const u4*>(sb + (kN - R + r) * kL);
+      v[r][0] = __builtin_nontemporal_load(p);
+      v[r][1] = __builtin_nontemporal_load(p + 64);
+    }
+    u4 a = {0u, 0u, 0u, 0u}, c = a;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      a ^= v[r][0];
+      c ^= v[r][1];
+    }
+    if (PRED || stats) {
+      const uint64_t d = rt() - t_go;  // after the XOR: the loads are back
+      est = est ? (3 * est + d) / 4 : d;
+      busy += d;
+      ++ntask;
+    }
+    if (nb == 0) tfirst = t;
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+      if (i == nb) {
+#pragma unroll
+        for (int o = 0; o < W; ++o) {
+          oa[i][o] = a + static_cast<uint32_t>(o);
+          ob[i][o] = c + static_cast<uint32_t>(o);
+        }
+      }
+    ++nb;
+  }
+  flush();
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], static_cast<unsigned long long>(busy));
+    atomicAdd(&stats[1], static_cast<unsigned long long>(ntask));
+  }
+}
+
 struct Variant {
   std::string name;
   double bytes;
@@ -244,8 +332,57 @@ struct Variant {
   std::vector<float> ms;
 };
 
+// calib mode: launch the register-phased kernel `launches` times, each period
+// P = slack * B * (mean read-phase task time of the previous launch) / (1 - f),
+// write window W = 1.25 * f * P, f = the write share of the mix's time at the
+// read / write peaks; one JSON line per launch.
+template <int R, int W, int B>
+void calib(uint8_t* base, unsigned grid, double slack, int launches, double f) {
+  unsigned long long* st = nullptr;
+  CK(hipMalloc(&st, 2 * sizeof(unsigned long long)));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  double tau = 0;
+  uint64_t P = 1000 * B;  // first guess: 10 us per task
+  for (int l = 0; l < launches; ++l) {
+    if (tau > 0) P = static_cast<uint64_t>(slack * B * tau / (1 - f));
+    const uint64_t Wt = static_cast<uint64_t>(1.25 * f * P);
+    CK(hipMemset(st, 0, 2 * sizeof(unsigned long long)));
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL((phased_sw_kernel<R, W, B, false>), dim3(grid), dim3(256), 0, 0, base, P, Wt, st);
+    CK(hipGetLastError());
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    unsigned long long h[2];
+    CK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
+    tau = h[1] ? static_cast<double>(h[0]) / h[1] : 0;
+    printf("{\"calib\": \"%dr%dw_b%d\", \"slack\": %.2f, \"launch\": %d, \"P\": %llu, \"W\": %llu, \"ms\": %.4f, "
+           "\"GBps\": %.1f, \"tau_ticks\": %.1f}\n",
+           R, W, B, slack, l, (unsigned long long)P, (unsigned long long)Wt, ms,
+           static_cast<double>(R + W) * kS * kL / 1e6 / ms, tau);
+  }
+  CK(hipFree(st));
+}
+
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 7;
+  if (argc > 2 && std::string(argv[2]) == "calib") {
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    uint8_t* base = nullptr;
+    CK(hipMalloc(&base, kS * kN * kL));
+    CK(hipMemset(base, 0x3C, kS * kN * kL));
+    const double f_dec = (1 / 6.1) / (10 / 6.8 + 1 / 6.1), f_enc = (4 / 6.1) / (10 / 6.8 + 4 / 6.1);
+    for (double slack : {1.0, 1.2, 1.4, 1.7, 2.0, 2.4}) {
+      calib<10, 1, 16>(base, 2 * cus, slack, reps, f_dec);
+      calib<10, 4, 5>(base, 2 * cus, slack, reps, f_enc);
+    }
+    CK(hipFree(base));
+    return 0;
+  }
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const unsigned grid = 2 * cus;
@@ -279,30 +416,36 @@ int main(int argc, char** argv) {
                   hipLaunchKernelGGL((phased_kernel<R, W, B>), dim3(grid), dim3(256), 0, 0, base,             \
                                      static_cast<uint64_t>(PER), static_cast<uint64_t>(WW));                  \
                 }, {}})
-  P(10, 1, 8, 5600, 700);
-  P(10, 1, 8, 6000, 700);
-  P(10, 1, 8, 6000, 900);
-  P(10, 1, 8, 6400, 700);
-  P(10, 1, 8, 6400, 900);
-  P(10, 1, 8, 6800, 900);
-  P(10, 1, 8, 7200, 1100);
-  P(10, 1, 10, 7000, 900);
-  P(10, 1, 10, 7600, 1000);
-  P(10, 1, 10, 8000, 1100);
-  P(10, 1, 10, 8400, 1200);
 #define Q(R, W, B, PER, WW)                                                                                 \
   vs.push_back({"q" #R "r" #W "w_b" #B "_P" #PER "_W" #WW, (R + W) * row, [=] {                            \
                   hipLaunchKernelGGL((phased_reg_kernel<R, W, B>), dim3(grid), dim3(256), 0, 0, base,         \
                                      static_cast<uint64_t>(PER), static_cast<uint64_t>(WW));                  \
                 }, {}})
-  Q(10, 1, 8, 6400, 900);
-  Q(10, 1, 8, 6800, 1000);
-  Q(10, 4, 4, 3200, 1000);
-  Q(10, 4, 4, 3600, 1200);
-  Q(10, 4, 4, 4000, 1400);
-  Q(10, 4, 6, 4800, 1500);
-  Q(10, 4, 6, 5400, 1700);
-  Q(10, 4, 6, 6000, 1900);
+#define SW(R, W, B, PER, WW)                                                                                \
+  vs.push_back({"s" #R "r" #W "w_b" #B "_P" #PER "_W" #WW, (R + W) * row, [=] {                            \
+                  hipLaunchKernelGGL((phased_sw_kernel<R, W, B>), dim3(grid), dim3(256), 0, 0, base,          \
+                                     static_cast<uint64_t>(PER), static_cast<uint64_t>(WW));                  \
+                }, {}})
+#define SP(R, W, B, PER, WW)                                                                                \
+  vs.push_back({"t" #R "r" #W "w_b" #B "_P" #PER "_W" #WW, (R + W) * row, [=] {                            \
+                  hipLaunchKernelGGL((phased_sw_kernel<R, W, B, true>), dim3(grid), dim3(256), 0, 0, base,    \
+                                     static_cast<uint64_t>(PER), static_cast<uint64_t>(WW));                  \
+                }, {}})
+  SW(10, 4, 5, 4800, 1500);
+  SP(10, 4, 5, 3600, 1100);
+  SP(10, 4, 5, 4000, 1200);
+  SP(10, 4, 5, 4400, 1300);
+  SP(10, 4, 5, 4800, 1450);
+  SP(10, 4, 5, 5200, 1550);
+  SP(10, 4, 5, 5600, 1700);
+  SP(10, 4, 5, 6000, 1800);
+  SW(10, 1, 16, 11000, 1500);
+  SP(10, 1, 16, 8000, 1000);
+  SP(10, 1, 16, 9000, 1100);
+  SP(10, 1, 16, 10000, 1200);
+  SP(10, 1, 16, 11000, 1300);
+  SP(10, 1, 16, 12000, 1450);
+  SP(10, 1, 16, 13000, 1550);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
