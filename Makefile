@@ -22,7 +22,13 @@ JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
             tests/cpp/copy_pool_test
 
-all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS)
+TOOLS    := tools/host_call_rate
+
+all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
+
+# The synchronous C-ABI call rate (bench.py's host_calls leg, profiles/r05/).
+tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build
@@ -164,6 +170,6 @@ tsan: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
 	@cat $(TSAN_LOG)/tsan_run.log
 
 clean:
-	rm -rf build $(LIB) $(ORACLE) $(JNI) $(HARNESS)
+	rm -rf build $(LIB) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
 
 .PHONY: all tsan clean asan

@@ -110,6 +110,20 @@ const char* hrs_last_error(const hrs_codec* codec);
 const char* hrs_last_kernel(const hrs_codec* codec);
 const char* hrs_version(void);
 
+/* ---- device set (SURVEY §5 "engine env/config for device set"; §8(e)) ----
+ * The reference creates one codec per Encoder / Decoder through
+ * Codec.createErasureCode -> ReflectionUtils.newInstance(class, conf) -> init
+ * (hadoop-hdfs/.../io/hops/erasure_coding/Codec.java:200-213). A binding picks
+ * the GPU of each handle with hrs_opts.device (the Java classes: round robin
+ * over the conf key hdfs.raid.hip.devices). */
+
+/* HIP devices visible to this process (HIP_VISIBLE_DEVICES applies); 0 if the
+ * HIP runtime finds none. Valid ordinals for hrs_opts.device are [0, count). */
+int hrs_device_count(void);
+/* Device ordinal a handle runs on (HRS_DEVICE_NONE for a host-only handle,
+ * -1 for NULL). */
+int hrs_codec_device(const hrs_codec* codec);
+
 /* ErasureCode.stripeSize()/paritySize()/symbolSize() (ReedSolomonCode.java:213-226). */
 int hrs_stripe_size(const hrs_codec* codec);
 int hrs_parity_size(const hrs_codec* codec);
@@ -301,6 +315,28 @@ hrs_status hrs_decode_batch_host(hrs_codec* codec, const uint8_t* stripes, size_
  * H2D and the p parity rows D2H. */
 hrs_status hrs_encode_batch_host(hrs_codec* codec, uint8_t* stripes, size_t row_stride, size_t stripe_stride,
                                  size_t len, size_t nstripes);
+
+/* The two host batches above over a device set: codecs[0..ncodecs) are
+ * distinct handles of one code (same family, stripe and parity size; SRC:
+ * same layout), each created on the device it should use (hrs_opts.device;
+ * a device may appear more than once). The stripes are split into ncodecs
+ * contiguous ranges of equal size (+-1 stripe), range i = stripes
+ * [i * nstripes / ncodecs, (i + 1) * nstripes / ncodecs), and range i runs as
+ * one hrs_*_batch_host call of codecs[i] on its own host thread (range 0 on
+ * the caller's), so every device moves its own share over its own host link
+ * (contiguous stripe ranges, one host thread and stream per
+ * device, no data exchange between devices). Same layout, semantics and
+ * results as the single-handle call; synchronous. On failure the first
+ * failing range's status is returned and its message is recorded on
+ * codecs[0] (hrs_last_error(codecs[0]); hrs_last_error(NULL) for a set
+ * rejected before any range ran with a NULL codecs array). The handles must
+ * not be used by other threads during the call. */
+hrs_status hrs_decode_batch_host_multi(hrs_codec* const* codecs, int ncodecs, const uint8_t* stripes,
+                                       size_t row_stride, size_t stripe_stride, const int* erased, int max_erased,
+                                       uint8_t* out, size_t out_row_stride, size_t out_stripe_stride, size_t len,
+                                       size_t nstripes);
+hrs_status hrs_encode_batch_host_multi(hrs_codec* const* codecs, int ncodecs, uint8_t* stripes, size_t row_stride,
+                                       size_t stripe_stride, size_t len, size_t nstripes);
 
 /* Generic GF(2^8) matrix x rows: out_o = XOR_i m[o * nin + i] * in_i (m on
  * the host, row-major nout x nin). Used with coding matrices broadcast over

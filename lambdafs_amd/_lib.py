@@ -41,6 +41,7 @@ EXPORTS = (
     "hrs_encode_crc_dev", "hrs_decode_crc_dev", "hrs_decode_batch_host", "hrs_encode_batch_host",
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
     "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_wait", "hrs_release",
+    "hrs_device_count", "hrs_codec_device", "hrs_decode_batch_host_multi", "hrs_encode_batch_host_multi",
 )
 # include/hrs_probe.h, exported by libhrs_probe.so
 PROBE_EXPORTS = ("hrs_probe_stream", "hrs_probe_rows")
@@ -104,6 +105,10 @@ def lib():
         "hrs_decode_crc_dev": ([P, PP, S, PP, S, IP, I, IP, I, S, S, P, P, P], I),
         "hrs_decode_batch_host": ([P, P, S, S, P, I, P, S, S, S, S], I),
         "hrs_encode_batch_host": ([P, P, S, S, S, S], I),
+        "hrs_decode_batch_host_multi": ([PP, I, P, S, S, P, I, P, S, S, S, S], I),
+        "hrs_encode_batch_host_multi": ([PP, I, P, S, S, S, S], I),
+        "hrs_device_count": ([], I),
+        "hrs_codec_device": ([P], I),
         "hrs_encode_submit": ([P, PP, S, I, ctypes.POINTER(ctypes.c_uint64)], I),
         "hrs_decode_submit": ([P, PP, IP, I, IP, I, IP, I, S, I, ctypes.POINTER(ctypes.c_uint64)], I),
         "hrs_collect": ([P, ctypes.c_uint64, PP, P], I),

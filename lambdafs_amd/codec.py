@@ -97,6 +97,7 @@ class Codec:
         if impl is None:
             raise ClassNotFoundException(name)
         code = impl()
+        code.setConf(conf)  # ReflectionUtils.newInstance(erasureCode, conf): Configurable codecs get conf
         code.init(self)
         return code
 

@@ -83,6 +83,8 @@ hrs_status create_impl(int code, int stripe_size, int parity_size, int src_s, co
     for (int r : opts->reserved)
       if (r != 0) return fail(nullptr, HRS_EINVAL, "hrs_opts.reserved must be zero");
   int dev = opts ? opts->device : -1;
+  if (dev < -1 && dev != HRS_DEVICE_NONE)
+    return fail(nullptr, HRS_EDEVICE, "no HIP device %d (ordinals are >= 0; -1 = current device)", dev);
   if (dev == HRS_DEVICE_NONE) {  // host-only handle: matrices and locations, no coding
     auto* c = new hrs_codec();
     c->device = HRS_DEVICE_NONE;
@@ -96,8 +98,8 @@ hrs_status create_impl(int code, int stripe_size, int parity_size, int src_s, co
   }
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
-  if (e != hipSuccess || dev >= ndev)
-    return fail(nullptr, HRS_EDEVICE, "no HIP device %d (%s)", dev, hipGetErrorString(e));
+  if (e != hipSuccess) return fail(nullptr, HRS_EDEVICE, "no HIP device %d (%s)", dev, hipGetErrorString(e));
+  if (dev >= ndev) return fail(nullptr, HRS_EDEVICE, "no HIP device %d (%d visible)", dev, ndev);
   auto* c = new hrs_codec();
   c->device = dev;
   init_code(c, code, stripe_size, parity_size, src_s);
@@ -217,6 +219,17 @@ void hrs_destroy(hrs_codec* c) {
 const char* hrs_last_error(const hrs_codec* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
 
 const char* hrs_last_kernel(const hrs_codec* c) { return c ? c->last_kernel.c_str() : ""; }
+
+int hrs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int hrs_codec_device(const hrs_codec* c) { return c ? c->device : -1; }
 
 int hrs_stripe_size(const hrs_codec* c) { return c ? c->k : -1; }
 int hrs_parity_size(const hrs_codec* c) { return c ? c->p : -1; }

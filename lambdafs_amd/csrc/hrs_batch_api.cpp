@@ -10,6 +10,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hrs.h"
@@ -517,6 +518,68 @@ hrs_status zero_copy_batch(hrs_codec* c, const BatchPlanSet& ps, const uint8_t* 
   return e == hipSuccess ? HRS_OK : hip_fail(c, e, "hipStreamSynchronize");
 }
 
+// ---------------------------------------------- device sets (hrs_*_multi)
+// contiguous stripe ranges, one host thread per device, no data
+// exchange. Each range is an ordinary single-handle host batch; the handles
+// are independent (their own slots, streams and staging), so the ranges run
+// concurrently with no shared state beyond the process-wide copy pool, which
+// takes batches from every open call in turn.
+
+hrs_status check_device_set(hrs_codec* const* cs, int nc) {
+  if (!cs || nc < 1) return fail(nullptr, HRS_EINVAL, "device set: need at least one codec");
+  for (int i = 0; i < nc; ++i)
+    if (!cs[i]) return fail(cs[0] ? cs[0] : nullptr, HRS_EINVAL, "device set: codecs[%d] is NULL", i);
+  hrs_codec* c0 = cs[0];
+  if (nc > 1024) return fail(c0, HRS_EINVAL, "device set: %d codecs (at most 1024)", nc);
+  for (int i = 0; i < nc; ++i) {
+    const hrs_codec* c = cs[i];
+    if (c->kind != c0->kind || c->k != c0->k || c->p != c0->p || c->src_s != c0->src_s)
+      return fail(c0, HRS_EINVAL, "device set: codecs[%d] is another code than codecs[0]", i);
+    for (int j = 0; j < i; ++j)
+      if (cs[j] == c) return fail(c0, HRS_EINVAL, "device set: codecs[%d] and codecs[%d] are one handle", j, i);
+  }
+  for (int i = 0; i < nc; ++i)
+    if (cs[i]->device < 0) return fail(c0, HRS_EDEVICE, "device set: codecs[%d] is a host-only handle", i);
+  return HRS_OK;
+}
+
+// Runs f(codec, first stripe, stripe count) for each member's range on its
+// own thread (member 0 on the caller's); returns the first failing member's
+// status with its message moved to codecs[0].
+template <typename F>
+hrs_status run_device_set(hrs_codec* const* cs, int nc, size_t nstripes, F f) {
+  std::vector<hrs_status> st(nc, HRS_OK);
+  auto lo = [&](int i) { return static_cast<size_t>((static_cast<unsigned __int128>(nstripes) * i) / nc); };
+  auto member = [&](int i) {
+    const size_t a = lo(i), b = lo(i + 1);
+    if (b > a) st[i] = f(cs[i], a, b - a);
+  };
+  std::vector<std::thread> th;
+  th.reserve(nc);
+  int inline_from = nc;  // members a thread could not be started for run here
+  for (int i = 1; i < nc; ++i) {
+    try {
+      th.emplace_back(member, i);
+    } catch (const std::exception&) {
+      inline_from = i;
+      break;
+    }
+  }
+  member(0);
+  for (int i = inline_from; i < nc; ++i) member(i);
+  for (auto& t : th) t.join();
+  for (int i = 0; i < nc; ++i)
+    if (st[i] != HRS_OK) {
+      if (i > 0) {
+        const std::string msg = cs[i]->err;
+        fail(cs[0], st[i], "device set member %d (device %d), stripes [%zu, %zu): %s", i, cs[i]->device, lo(i),
+             lo(i + 1), msg.c_str());
+      }
+      return st[i];
+    }
+  return HRS_OK;
+}
+
 }  // namespace hrs::api
 
 using namespace hrs::api;
@@ -669,6 +732,33 @@ hrs_status hrs_encode_batch_host(hrs_codec* c, uint8_t* stripes, size_t row_stri
   // parity rows 0..p-1 of each stripe are written in place
   return drain_hbatch(c, host_batch(c, stripes, row_stride, stripe_stride, c->n, stripes, row_stride, stripe_stride,
                                     p, len, nstripes, reads, compute, writes));
+}
+
+hrs_status hrs_decode_batch_host_multi(hrs_codec* const* codecs, int ncodecs, const uint8_t* stripes,
+                                       size_t row_stride, size_t stripe_stride, const int* erased, int max_erased,
+                                       uint8_t* out, size_t out_row_stride, size_t out_stripe_stride, size_t len,
+                                       size_t nstripes) {
+  hrs_status st = check_device_set(codecs, ncodecs);
+  if (st != HRS_OK) return st;
+  if (!stripes || !out || max_erased < 0 || max_erased > hrs::kMaxOut || (max_erased > 0 && !erased))
+    return fail(codecs[0], HRS_EINVAL, "bad batch decode arguments (max_erased must be in [0, %d])", hrs::kMaxOut);
+  if (nstripes == 0 || len == 0 || max_erased == 0) return HRS_OK;
+  return run_device_set(codecs, ncodecs, nstripes, [&](hrs_codec* c, size_t s0, size_t ns) {
+    return hrs_decode_batch_host(c, stripes + s0 * stripe_stride, row_stride, stripe_stride,
+                                 erased + s0 * static_cast<size_t>(max_erased), max_erased,
+                                 out + s0 * out_stripe_stride, out_row_stride, out_stripe_stride, len, ns);
+  });
+}
+
+hrs_status hrs_encode_batch_host_multi(hrs_codec* const* codecs, int ncodecs, uint8_t* stripes, size_t row_stride,
+                                       size_t stripe_stride, size_t len, size_t nstripes) {
+  hrs_status st = check_device_set(codecs, ncodecs);
+  if (st != HRS_OK) return st;
+  if (!stripes) return fail(codecs[0], HRS_EINVAL, "stripes is NULL");
+  if (nstripes == 0 || len == 0) return HRS_OK;
+  return run_device_set(codecs, ncodecs, nstripes, [&](hrs_codec* c, size_t s0, size_t ns) {
+    return hrs_encode_batch_host(c, stripes + s0 * stripe_stride, row_stride, stripe_stride, len, ns);
+  });
 }
 
 }  // extern "C"

@@ -148,7 +148,7 @@ hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStr
   const uint64_t per_block = kCrcBlockThreads / 64;
   uint64_t g = (waves + per_block - 1) / per_block;
   if (g > static_cast<uint64_t>(cus)) g = cus;
-  if (g == 0) g = 1;
+  g = capped_grid(g);  // zero-copy calls cap it (hrs::GridCap)
   const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
   auto k = aligned ? crc_window_kernel<true> : crc_window_kernel<false>;
   note_kernel(aligned ? "crc_window_kernel<true>" : "crc_window_kernel<false>");

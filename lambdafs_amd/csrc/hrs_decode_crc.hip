@@ -214,7 +214,7 @@ hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
     const uint64_t per_block = threads / 64;
     uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
     if (g > static_cast<uint64_t>(cus)) g = cus;
-    if (g == 0) g = 1;
+    g = capped_grid(g);  // zero-copy calls cap it (hrs::GridCap)
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(threads), shm, s, dc);
     return hipGetLastError();
   } else {
@@ -227,7 +227,7 @@ hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
     constexpr uint64_t per_block = kDecCrcThreads / 64;
     uint64_t g = (d.r.ntasks + per_block - 1) / per_block;
     if (g > static_cast<uint64_t>(cus)) g = cus;
-    if (g == 0) g = 1;
+    g = capped_grid(g);  // zero-copy calls cap it (hrs::GridCap)
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g)), dim3(kDecCrcThreads), shm, s, dc);
     return hipGetLastError();
   }

@@ -323,7 +323,7 @@ hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   const uint64_t per_block = k.threads / 64;
   uint64_t g = (ntasks + per_block - 1) / per_block;
   if (g > static_cast<uint64_t>(cus)) g = cus;
-  if (g == 0) g = 1;
+  g = capped_grid(g);  // zero-copy calls cap it (hrs::GridCap)
   hipLaunchKernelGGL(k.k, dim3(static_cast<unsigned>(g)), dim3(k.threads), shm, s, with_order(a, kOrderFusedEncode));
   return hipGetLastError();
 }

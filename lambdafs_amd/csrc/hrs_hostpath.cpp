@@ -129,7 +129,6 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     if (crc.mode == kCrcOutputs) return apply_crc_one_pass(c, nout, nlive, lj);
     return true;
   };
-  hrs::GridCap cap(zc_ok ? zero_copy_blocks() : 0u);
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
   size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
@@ -163,6 +162,9 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
       if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
     pool.run(jobs);
     const bool zc = zc_chunk(lj);
+    // only zero-copy chunks cap their grid (the link bounds them); a chunk
+    // sent back to the copy engine runs on device memory with the full grid
+    hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
     if (nlive > 0 && !zc) {
       hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
       if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");

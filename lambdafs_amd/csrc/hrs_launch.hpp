@@ -92,7 +92,10 @@ inline int blocks_per_cu(int dflt = 2) {
 // Zero-copy launches (kernels reading and writing pinned host memory across
 // the host link, hrs_batch_api.cpp / hrs_hostpath.cpp) cap their grid: the
 // link, not the CUs, bounds them, so a capped grid leaves the rest of the chip
-// to other work. Set for the calling thread by a GridCap around the launch.
+// to other work. Set for the calling thread by a GridCap around the launch;
+// every launcher sizes its grid through capped_grid (stream_grid, grid_for,
+// and the fused / CRC launchers, whose 1,024- or 512-thread blocks take one
+// CU each, so the cap in blocks is a cap in CUs there).
 inline thread_local unsigned t_grid_cap = 0;
 
 struct GridCap {

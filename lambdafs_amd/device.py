@@ -191,6 +191,47 @@ def encode_batch_host(code, stripes):
     code._check(_lib.lib().hrs_encode_batch_host(code._handle(), sp, sstr[1], sstr[0], sshape[2], sshape[0]))
 
 
+def _codec_array(codes):
+    codes = list(codes)
+    if not codes:
+        raise ValueError("a device set needs at least one codec")
+    return codes, ptr_array([c._handle().value for c in codes])
+
+
+def decode_batch_host_multi(codes, stripes, erased, out):
+    """hrs_decode_batch_host_multi: decode_batch_host over a device set. `codes`
+    are distinct codecs of one code, each on the device it should use; the
+    stripes split into len(codes) contiguous ranges, one per codec, run on
+    their own host threads (one host link per device)."""
+    codes, arr = _codec_array(codes)
+    n = codes[0].stripeSize() + codes[0].paritySize()
+    sp, sshape, sstr = _host_ptr(stripes, "stripes")
+    op, oshape, ostr = _host_ptr(out, "out", writable=True)
+    e = np.ascontiguousarray(np.asarray(erased, dtype=np.int32))
+    if len(sshape) != 3 or sshape[1] != n or sstr[2] != 1:
+        raise ValueError(f"stripes must be [S, {n}, L] with unit byte stride")
+    S, L = sshape[0], sshape[2]
+    if e.ndim != 2 or e.shape[0] != S:
+        raise ValueError("erased must be [S, E]")
+    if len(oshape) != 3 or tuple(oshape) != (S, e.shape[1], L) or ostr[2] != 1:
+        raise ValueError("out must be [S, E, L]")
+    _lib.check(_lib.lib().hrs_decode_batch_host_multi(
+        arr, len(codes), sp, sstr[1], sstr[0], e.ctypes.data, e.shape[1], op, ostr[1], ostr[0], L, S),
+        codes[0]._h)
+
+
+def encode_batch_host_multi(codes, stripes):
+    """hrs_encode_batch_host_multi: encode_batch_host over a device set
+    (contiguous stripe ranges, one per codec, each on its own host thread)."""
+    codes, arr = _codec_array(codes)
+    n = codes[0].stripeSize() + codes[0].paritySize()
+    sp, sshape, sstr = _host_ptr(stripes, "stripes", writable=True)
+    if len(sshape) != 3 or sshape[1] != n or sstr[2] != 1:
+        raise ValueError(f"stripes must be [S, {n}, L] with unit byte stride")
+    _lib.check(_lib.lib().hrs_encode_batch_host_multi(arr, len(codes), sp, sstr[1], sstr[0], sshape[2], sshape[0]),
+               codes[0]._h)
+
+
 def apply_rows(code, matrix, in_rows, out_rows):
     """out_o = XOR_i matrix[o, i] * in_i over S stripes (matrix: host uint8 [nout, nin]).
     Used with coding matrices broadcast over RCCL (bench.py --gpus N)."""

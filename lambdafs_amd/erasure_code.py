@@ -151,20 +151,42 @@ class _HipErasureCode(ErasureCode):
         self._h = None
         self._k = self._p = 0
         self._device = device
+        self._conf = None
         self.zero_inputs_after_encode = zero_inputs_after_encode
         if stripeSize is not None:
             self._init(stripeSize, paritySize)
 
     # -- lifecycle
+    def setConf(self, conf):
+        """Configurable.setConf: Codec.createErasureCode hands the conf to the
+        new instance before init (ReflectionUtils.newInstance, Codec.java:209-211).
+        Unless the instance was built for an explicit device, init then takes
+        the next device of `hdfs.raid.hip.devices` (devset.py)."""
+        self._conf = conf
+
+    def getConf(self):
+        return self._conf
+
+    def device(self):
+        """Device ordinal the handle runs on (hrs_codec_device)."""
+        return int(_lib.lib().hrs_codec_device(self._handle()))
+
     def init(self, codec):
         """ReedSolomonCode.init(Codec), ReedSolomonCode.java:48-54."""
         self._init(codec.stripeLength, codec.parityLength)
 
+    def _opts(self):
+        opts = _lib.HipOpts()
+        if self._device is None and self._conf is not None:
+            from .devset import pick_device
+            self._device = pick_device(self._conf)
+        opts.device = -1 if self._device is None else int(self._device)
+        return opts
+
     def _init(self, k, p):
         L = _lib.lib()
         self.close()
-        opts = _lib.HipOpts()
-        opts.device = -1 if self._device is None else int(self._device)
+        opts = self._opts()
         h = ctypes.c_void_p()
         check(L.hrs_create_code(self.CODE_KIND, int(k), int(p), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
@@ -506,7 +528,11 @@ class HipReedSolomonCode(_HipErasureCode):
 
     def decode(self, data, erasedLocations, erasedValues, locationsToRead=None, locationsNotToRead=None):
         """3-arg ReedSolomonCode.decode (:127-142) or 5-arg (:144-166).
-        Like the Java, zeroes data at the locations treated as erased."""
+        Like the Java, zeroes data at the locations treated as erased, and
+        writes erasedValues[i] only when erasedLocations[i] is one of the
+        locations decoded (locationsNotToRead): the Java copies recovered
+        values by matching locations (:158-165) and leaves any other entry as
+        the caller passed it."""
         n = self._k + self._p
         if len(data) != n or len(erasedValues) != len(erasedLocations):
             raise ValueError("data/erasedValues length mismatch")
@@ -525,8 +551,10 @@ class HipReedSolomonCode(_HipErasureCode):
         if not erasedLocations:
             return
         self.decodeBulk(rows, outs, list(erasedLocations), toread, ntr)
+        decoded = set(ntr)
         for i in range(len(erasedLocations)):
-            erasedValues[i] = int(outs[i][0])
+            if erasedLocations[i] in decoded:
+                erasedValues[i] = int(outs[i][0])
 
 
 
@@ -624,8 +652,7 @@ class HipSimpleRegeneratingCode(_HipErasureCode):
     def _init(self, k, p):
         L = _lib.lib()
         self.close()
-        opts = _lib.HipOpts()
-        opts.device = -1 if self._device is None else int(self._device)
+        opts = self._opts()
         h = ctypes.c_void_p()
         check(L.hrs_create_src(int(k), int(p), self._src_in, ctypes.byref(opts), ctypes.byref(h)))
         self._h = h

@@ -9,11 +9,41 @@
 package io.hops.erasure_coding;
 
 import java.io.IOException;
+import org.apache.hadoop.conf.Configurable;
+import org.apache.hadoop.conf.Configuration;
 
-public class HipNativeReedSolomonCode extends ErasureCode {
+public class HipNativeReedSolomonCode extends ErasureCode implements Configurable {
   private long nativeCodec;
   private int stripeSize;
   private int paritySize;
+
+  // Configurable: Codec.createErasureCode hands the conf over before init
+  // (ReflectionUtils.newInstance, Codec.java:209-211); init then takes the
+  // next device of hdfs.raid.hip.devices (HipDevices).
+  private Configuration conf;
+
+  @Override
+  public void setConf(Configuration conf) {
+    this.conf = conf;
+  }
+
+  @Override
+  public Configuration getConf() {
+    return conf;
+  }
+
+  /** The HIP device this instance runs on. */
+  public int device() {
+    return HrsNative.device(nativeCodec);
+  }
+
+  private static long create(int code, int k, int p, int device) {
+    try {
+      return HrsNative.create(code, k, p, device);
+    } catch (IOException e) {  // no such device: init(Codec) declares no IOException
+      throw new RuntimeException(e);
+    }
+  }
 
   public HipNativeReedSolomonCode() {
   }
@@ -23,7 +53,7 @@ public class HipNativeReedSolomonCode extends ErasureCode {
     release();
     stripeSize = codec.stripeLength;
     paritySize = codec.parityLength;
-    nativeCodec = HrsNative.create(HrsNative.CODE_NRS, stripeSize, paritySize);
+    nativeCodec = create(HrsNative.CODE_NRS, stripeSize, paritySize, HipDevices.pick(conf));
   }
 
   @Override

@@ -14,11 +14,41 @@ package io.hops.erasure_coding;
 
 import java.io.IOException;
 import java.util.Arrays;
+import org.apache.hadoop.conf.Configurable;
+import org.apache.hadoop.conf.Configuration;
 
-public class HipReedSolomonCode extends ErasureCode {
+public class HipReedSolomonCode extends ErasureCode implements Configurable {
   private long nativeCodec;  // hrs_codec*, owned (cf. jni_common.c:35-70 "nativeCoder")
   private int stripeSize;
   private int paritySize;
+
+  // Configurable: Codec.createErasureCode hands the conf over before init
+  // (ReflectionUtils.newInstance, Codec.java:209-211); init then takes the
+  // next device of hdfs.raid.hip.devices (HipDevices).
+  private Configuration conf;
+
+  @Override
+  public void setConf(Configuration conf) {
+    this.conf = conf;
+  }
+
+  @Override
+  public Configuration getConf() {
+    return conf;
+  }
+
+  /** The HIP device this instance runs on. */
+  public int device() {
+    return HrsNative.device(nativeCodec);
+  }
+
+  private static long create(int code, int k, int p, int device) {
+    try {
+      return HrsNative.create(code, k, p, device);
+    } catch (IOException e) {  // no such device: init(Codec) declares no IOException
+      throw new RuntimeException(e);
+    }
+  }
 
   public HipReedSolomonCode() {
   }
@@ -37,7 +67,7 @@ public class HipReedSolomonCode extends ErasureCode {
     release();
     this.stripeSize = stripeSize;
     this.paritySize = paritySize;
-    this.nativeCodec = HrsNative.create(HrsNative.CODE_RS, stripeSize, paritySize);  // throws IllegalArgumentException / RuntimeException
+    this.nativeCodec = create(HrsNative.CODE_RS, stripeSize, paritySize, HipDevices.pick(conf));
   }
 
   /** Same result as ReedSolomonCode.encodeBulk (ReedSolomonCode.java:103-125). */
@@ -183,8 +213,17 @@ public class HipReedSolomonCode extends ErasureCode {
     } catch (IOException e) {
       throw new RuntimeException(e);
     }
+    // ReedSolomonCode.java:158-165 copies a recovered value only where
+    // erasedLocations[i] is one of locationsNotToRead; any other entry of
+    // erasedValues keeps what the caller passed (the engine's zero row for it
+    // is not copied).
     for (int i = 0; i < erasedLocations.length; i++) {
-      erasedValues[i] = out[i][0] & 0xFF;
+      for (int loc : locationsNotToRead) {
+        if (erasedLocations[i] == loc) {
+          erasedValues[i] = out[i][0] & 0xFF;
+          break;
+        }
+      }
     }
   }
 

@@ -12,11 +12,41 @@ import java.io.IOException;
 import java.util.ArrayList;
 import java.util.List;
 import org.json.JSONException;
+import org.apache.hadoop.conf.Configurable;
+import org.apache.hadoop.conf.Configuration;
 
-public class HipSimpleRegeneratingCode extends ErasureCode {
+public class HipSimpleRegeneratingCode extends ErasureCode implements Configurable {
   private long nativeCodec;
   private int stripeSize;
   private int paritySize;
+
+  // Configurable: Codec.createErasureCode hands the conf over before init
+  // (ReflectionUtils.newInstance, Codec.java:209-211); init then takes the
+  // next device of hdfs.raid.hip.devices (HipDevices).
+  private Configuration conf;
+
+  @Override
+  public void setConf(Configuration conf) {
+    this.conf = conf;
+  }
+
+  @Override
+  public Configuration getConf() {
+    return conf;
+  }
+
+  /** The HIP device this instance runs on. */
+  public int device() {
+    return HrsNative.device(nativeCodec);
+  }
+
+  private static long createSrc(int k, int p, int s, int device) {
+    try {
+      return HrsNative.createSrc(k, p, s, device);
+    } catch (IOException e) {  // no such device: init(Codec) declares no IOException
+      throw new RuntimeException(e);
+    }
+  }
 
   public HipSimpleRegeneratingCode() {
   }
@@ -32,7 +62,7 @@ public class HipSimpleRegeneratingCode extends ErasureCode {
     release();
     stripeSize = codec.stripeLength;
     paritySize = codec.parityLength;
-    nativeCodec = HrsNative.createSrc(stripeSize, paritySize, srcParities);
+    nativeCodec = createSrc(stripeSize, paritySize, srcParities, HipDevices.pick(conf));
   }
 
   @Override

@@ -6,10 +6,40 @@
 package io.hops.erasure_coding;
 
 import java.io.IOException;
+import org.apache.hadoop.conf.Configurable;
+import org.apache.hadoop.conf.Configuration;
 
-public class HipXORCode extends ErasureCode {
+public class HipXORCode extends ErasureCode implements Configurable {
   private long nativeCodec;
   private int stripeSize;
+
+  // Configurable: Codec.createErasureCode hands the conf over before init
+  // (ReflectionUtils.newInstance, Codec.java:209-211); init then takes the
+  // next device of hdfs.raid.hip.devices (HipDevices).
+  private Configuration conf;
+
+  @Override
+  public void setConf(Configuration conf) {
+    this.conf = conf;
+  }
+
+  @Override
+  public Configuration getConf() {
+    return conf;
+  }
+
+  /** The HIP device this instance runs on. */
+  public int device() {
+    return HrsNative.device(nativeCodec);
+  }
+
+  private static long create(int code, int k, int p, int device) {
+    try {
+      return HrsNative.create(code, k, p, device);
+    } catch (IOException e) {  // no such device: init(Codec) declares no IOException
+      throw new RuntimeException(e);
+    }
+  }
 
   public HipXORCode() {
   }
@@ -19,7 +49,7 @@ public class HipXORCode extends ErasureCode {
     assert (codec.parityLength == 1);
     release();
     stripeSize = codec.stripeLength;
-    nativeCodec = HrsNative.create(HrsNative.CODE_XOR, codec.stripeLength, 1);
+    nativeCodec = create(HrsNative.CODE_XOR, codec.stripeLength, 1, HipDevices.pick(conf));
   }
 
   @Override

@@ -20,9 +20,19 @@ final class HrsNative {
   private HrsNative() {
   }
 
-  static native long create(int code, int stripeSize, int paritySize);
+  // hrs_create_code / hrs_create_src on HIP device `device` (-1 = the
+  // thread's current device; HipDevices.pick chooses it). A device that is
+  // not visible throws IOException (HRS_EDEVICE), bad geometry
+  // IllegalArgumentException.
+  static native long create(int code, int stripeSize, int paritySize, int device) throws IOException;
 
-  static native long createSrc(int stripeSize, int paritySize, int srcParitySize);
+  static native long createSrc(int stripeSize, int paritySize, int srcParitySize, int device) throws IOException;
+
+  // hrs_device_count: HIP devices visible to this JVM (HIP_VISIBLE_DEVICES applies)
+  static native int deviceCount();
+
+  // hrs_codec_device: the device a handle runs on
+  static native int device(long codec);
 
   static native void destroy(long codec);
 

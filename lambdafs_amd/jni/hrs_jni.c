@@ -192,11 +192,15 @@ static void close_frame(JNIEnv* env) { (void)(*env)->PopLocalFrame(env, NULL); }
 
 /* ------------------------------------------------------------ lifecycle */
 
-JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv* env, jclass cls, jint code, jint k,
-                                                                       jint p) {
-  (void)cls;
+/* The device a codec instance runs on (HipDevices.pick: round robin over
+ * hdfs.raid.hip.devices; -1 = the thread's current device). An ordinal that
+ * is not a visible device fails hrs_create with HRS_EDEVICE -> IOException. */
+static jlong create_on(JNIEnv* env, int code, jint k, jint p, int src, jint s, jint device) {
+  hrs_opts o;
+  memset(&o, 0, sizeof o);
+  o.device = device;
   hrs_codec* c = NULL;
-  hrs_status st = hrs_create_code(code, k, p, NULL, &c);
+  const hrs_status st = src ? hrs_create_src(k, p, s, &o, &c) : hrs_create_code(code, k, p, &o, &c);
   if (st != HRS_OK) {
     throw_status(env, st, NULL);
     return 0;
@@ -204,16 +208,30 @@ JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv* en
   return (jlong)(intptr_t)c;
 }
 
-JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_createSrc(JNIEnv* env, jclass cls, jint k, jint p,
-                                                                          jint s) {
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv* env, jclass cls, jint code, jint k,
+                                                                       jint p, jint device) {
   (void)cls;
-  hrs_codec* c = NULL;
-  hrs_status st = hrs_create_src(k, p, s, NULL, &c);
-  if (st != HRS_OK) {
-    throw_status(env, st, NULL);
-    return 0;
-  }
-  return (jlong)(intptr_t)c;
+  return create_on(env, code, k, p, 0, 0, device);
+}
+
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_createSrc(JNIEnv* env, jclass cls, jint k, jint p,
+                                                                          jint s, jint device) {
+  (void)cls;
+  return create_on(env, HRS_CODE_SRC, k, p, 1, s, device);
+}
+
+/* hrs_device_count: devices visible to this JVM (HIP_VISIBLE_DEVICES applies). */
+JNIEXPORT jint JNICALL Java_io_hops_erasure_1coding_HrsNative_deviceCount(JNIEnv* env, jclass cls) {
+  (void)env;
+  (void)cls;
+  return hrs_device_count();
+}
+
+/* hrs_codec_device: the ordinal a handle runs on. */
+JNIEXPORT jint JNICALL Java_io_hops_erasure_1coding_HrsNative_device(JNIEnv* env, jclass cls, jlong h) {
+  (void)cls;
+  hrs_codec* c = handle(env, h);
+  return c ? hrs_codec_device(c) : -1;
 }
 
 JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_destroy(JNIEnv* env, jclass cls, jlong h) {

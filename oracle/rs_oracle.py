@@ -191,11 +191,17 @@ def decode3(k, p, data, erased):
     return list(vals)[: len(erased)], list(d)[: len(data)]
 
 
-def decode5(k, p, data, erased, to_read, not_to_read):
+def decode5(k, p, data, erased, to_read, not_to_read, values=None, with_data=False):
+    """ReedSolomonCode.decode 5-arg (:144-166). `values` pre-fills erasedValues
+    (the Java leaves an entry whose location is not in not_to_read as the caller
+    passed it); with_data also returns `data` after the call (zeroed at
+    not_to_read by the 3-arg decode it runs)."""
     d = _ints(data)
-    vals = _ints([0] * len(erased))
+    vals = _ints(list(values) if values is not None else [0] * len(erased))
     lib().orc_rs_decode5(k, p, d, _ints(erased), len(erased), vals, _ints(to_read), len(to_read),
                          _ints(not_to_read), len(not_to_read))
+    if with_data:
+        return list(vals)[: len(erased)], list(d)[: len(data)]
     return list(vals)[: len(erased)]
 
 

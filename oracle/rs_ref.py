@@ -118,10 +118,11 @@ class ReedSolomonRef:
         solve_vandermonde(sig, vals, len(erased))
         return vals
 
-    def decode5(self, data, erased, to_read, not_to_read):
-        """ReedSolomonCode.java:144-166."""
+    def decode5(self, data, erased, to_read, not_to_read, values=None):
+        """ReedSolomonCode.java:144-166. `values` = the caller's erasedValues
+        (entries whose location is not in not_to_read are left as passed)."""
         recov = self.decode3(data, list(not_to_read))
-        out = [0] * len(erased)
+        out = list(values) if values is not None else [0] * len(erased)
         for i, e in enumerate(erased):
             for j, ntr in enumerate(not_to_read):
                 if e == ntr:

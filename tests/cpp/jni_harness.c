@@ -368,8 +368,10 @@ static void init_table(void) {
 
 /* ----------------------------------------------- the shim's entry points */
 
-JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv*, jclass, jint, jint, jint);
-JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_createSrc(JNIEnv*, jclass, jint, jint, jint);
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_create(JNIEnv*, jclass, jint, jint, jint, jint);
+JNIEXPORT jlong JNICALL Java_io_hops_erasure_1coding_HrsNative_createSrc(JNIEnv*, jclass, jint, jint, jint, jint);
+JNIEXPORT jint JNICALL Java_io_hops_erasure_1coding_HrsNative_deviceCount(JNIEnv*, jclass);
+JNIEXPORT jint JNICALL Java_io_hops_erasure_1coding_HrsNative_device(JNIEnv*, jclass, jlong);
 JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_destroy(JNIEnv*, jclass, jlong);
 JNIEXPORT jintArray JNICALL Java_io_hops_erasure_1coding_HrsNative_locationsToRead(JNIEnv*, jclass, jlong, jintArray);
 JNIEXPORT void JNICALL Java_io_hops_erasure_1coding_HrsNative_encode(JNIEnv*, jclass, jlong, jobjectArray,
@@ -492,9 +494,23 @@ static int cpu_checks(void) {
   EXPECT_THROWN("released handle", kISE, NS(locationsToRead)(env, NULL, 0, new_ints(1, e7)));
 
   /* create: engine status -> exception class */
-  EXPECT_THROWN("create RS(0,4)", kIAE, NS(create)(env, NULL, HRS_CODE_RS, 0, 4));
-  EXPECT_THROWN("create XOR(10,2)", kIAE, NS(create)(env, NULL, HRS_CODE_XOR, 10, 2));
-  EXPECT_THROWN("createSrc(10,4,5)", kIAE, NS(createSrc)(env, NULL, 10, 4, 5));
+  EXPECT_THROWN("create RS(0,4)", kIAE, NS(create)(env, NULL, HRS_CODE_RS, 0, 4, -1));
+  EXPECT_THROWN("create XOR(10,2)", kIAE, NS(create)(env, NULL, HRS_CODE_XOR, 10, 2, -1));
+  EXPECT_THROWN("createSrc(10,4,5)", kIAE, NS(createSrc)(env, NULL, 10, 4, 5, -1));
+  /* device set: an ordinal that is no visible device -> IOException (here
+   * none is visible; on the GPU box gpu_checks tries deviceCount() itself) */
+  {
+    jint nd = -1;
+    CALL("deviceCount", nd = NS(deviceCount)(env, NULL));
+    expect(nd >= 0 && !vm.pending, "deviceCount");
+    EXPECT_THROWN("create on device 4096", kIOE, NS(create)(env, NULL, HRS_CODE_RS, 10, 4, 4096));
+    EXPECT_THROWN("create on device -7", kIOE, NS(create)(env, NULL, HRS_CODE_RS, 10, 4, -7));
+    EXPECT_THROWN("createSrc on device 4096", kIOE, NS(createSrc)(env, NULL, 10, 6, 2, 4096));
+    jint dv = 0;
+    CALL("device of a host-only handle", dv = NS(device)(env, NULL, h));
+    expect(dv == HRS_DEVICE_NONE && !vm.pending, "device() of a host-only handle: %d", (int)dv);
+    EXPECT_THROWN("device of a released handle", kISE, NS(device)(env, NULL, 0));
+  }
   CALL("destroy(0)", NS(destroy)(env, NULL, 0));
   expect(!vm.pending, "destroy(0) threw");
 
@@ -592,13 +608,86 @@ static int cpu_checks(void) {
 
 static uint32_t zcrc(uint32_t c, const uint8_t* p, size_t n) { return (uint32_t)crc32(c, p, (uInt)n); }
 
+/* HipReedSolomonCode.decode 5-arg (lambdafs_amd/jni/HipReedSolomonCode.java),
+ * transcribed: zero data at locationsNotToRead, one-byte rows through
+ * HrsNative.decode, then copy out[i] only where erasedLocations[i] is one of
+ * locationsNotToRead (ReedSolomonCode.java:158-165). Compared with the
+ * oracle's ReedSolomonCode.decode on pre-filled erasedValues. */
+static void java_scalar_decode5(jlong h, int* data, int n, const int* erased, int ne, int* values, const int* ntr,
+                                int nn) {
+  for (int j = 0; j < nn; j++) data[ntr[j]] = 0;
+  jobjectArray rb = new_objs(n);
+  for (int i = 0; i < n; i++) {
+    jbyteArray b = new_bytes(1);
+    bytes_of(b)[0] = (uint8_t)data[i];
+    set_obj(rb, i, b);
+  }
+  jobjectArray out = rows(ne, 1, 0);
+  CALL("scalar decode5 (HrsNative.decode, 1-byte rows)",
+       NS(decode)(env, NULL, h, rb, out, new_ints(ne, erased), new_ints(0, NULL), new_ints(nn, ntr), 1));
+  for (int i = 0; i < ne; i++)
+    for (int j = 0; j < nn; j++)
+      if (erased[i] == ntr[j]) {
+        values[i] = bytes_of(row(out, i))[0];
+        break;
+      }
+}
+
+static void scalar_decode5_checks(jlong h, int k, int p) {
+  const int n = k + p;
+  uint64_t seed = 0x5CA1A7ull;
+  for (int it = 0; it < 24; it++) {
+    int data[64], dref[64], ntr[16], er[16], v[16], vref[16];
+    for (int i = 0; i < n; i++) data[i] = dref[i] = (int)(splitmix(&seed) & 0xFF);
+    /* not-to-read: 1..p distinct locations; erased: some of them plus 1-2 outside */
+    int nn = 1 + (int)(splitmix(&seed) % (uint64_t)p), ne = 0;
+    for (int j = 0; j < nn; j++) {
+      int loc, dup;
+      do {
+        loc = (int)(splitmix(&seed) % (uint64_t)n);
+        dup = 0;
+        for (int q = 0; q < j; q++) dup |= ntr[q] == loc;
+      } while (dup);
+      ntr[j] = loc;
+      if (splitmix(&seed) & 1) er[ne++] = loc;
+    }
+    for (int extra = 1 + (int)(splitmix(&seed) & 1), loc = 0; extra > 0 && loc < n; loc++) {
+      int in = 0;
+      for (int j = 0; j < nn; j++) in |= ntr[j] == loc;
+      if (!in && (splitmix(&seed) % 3) == 0) er[ne++] = loc, extra--;
+    }
+    if (ne == 0) continue;
+    for (int i = 0; i < ne; i++) v[i] = vref[i] = 0x40 + it + i; /* pre-filled erasedValues */
+    java_scalar_decode5(h, data, n, er, ne, v, ntr, nn);
+    orc_rs_decode5(k, p, dref, er, ne, vref, NULL, 0, ntr, nn);
+    int same = !vm.pending && memcmp(v, vref, sizeof(int) * (size_t)ne) == 0 &&
+               memcmp(data, dref, sizeof(int) * (size_t)n) == 0;
+    expect(same, "scalar decode5 round %d: erasedValues or data differ from ReedSolomonCode.decode", it);
+  }
+}
+
 static int gpu_checks(void) {
   const int k = 10, p = 4, n = 14;
   const jsize L = 1 << 20;
   jlong h = 0;
-  CALL("create RS(10,4)", h = NS(create)(env, NULL, HRS_CODE_RS, k, p));
+  /* device set: explicit ordinals as HipDevices.pick hands them out */
+  jint ndev = 0;
+  CALL("deviceCount", ndev = NS(deviceCount)(env, NULL));
+  expect(ndev >= 1 && !vm.pending, "deviceCount on the GPU box: %d", (int)ndev);
+  for (jint d = 0; d < ndev && d < 8; ++d) {
+    jlong hd = 0;
+    jint got = -1;
+    CALL("create on device d", hd = NS(create)(env, NULL, HRS_CODE_RS, k, p, d));
+    CALL("device()", got = hd ? NS(device)(env, NULL, hd) : -1);
+    expect(hd != 0 && got == d && !vm.pending, "create on device %d -> handle on %d", (int)d, (int)got);
+    if (hd) CALL("destroy", NS(destroy)(env, NULL, hd));
+  }
+  EXPECT_THROWN("create on device deviceCount()", kIOE, NS(create)(env, NULL, HRS_CODE_RS, k, p, ndev));
+  EXPECT_THROWN("createSrc on device deviceCount()", kIOE, NS(createSrc)(env, NULL, 10, 6, 2, ndev));
+  CALL("create RS(10,4)", h = NS(create)(env, NULL, HRS_CODE_RS, k, p, 0));
   expect(h != 0 && !vm.pending, "create RS(10,4) on the GPU: %s", vm.exc_msg);
   if (!h) return 1;
+  scalar_decode5_checks(h, k, p);
 
   /* encode vs oracle encodeBulk */
   jobjectArray in = rows(k, L, 7), out = rows(p, L, 0);
@@ -804,7 +893,7 @@ static int gpu_checks(void) {
   /* the other code families through the same shim */
   {
     jlong hx = 0;
-    CALL("create XOR", hx = NS(create)(env, NULL, HRS_CODE_XOR, 10, 1));
+    CALL("create XOR", hx = NS(create)(env, NULL, HRS_CODE_XOR, 10, 1, -1));
     jobjectArray xin = rows(10, 70000, 21), xout = rows(1, 70000, 0);
     CALL("xor encode", NS(encode)(env, NULL, hx, xin, xout, 70000));
     uint8_t* xr[10];
@@ -816,7 +905,7 @@ static int gpu_checks(void) {
     CALL("destroy XOR", NS(destroy)(env, NULL, hx));
 
     jlong hn = 0;
-    CALL("create NRS", hn = NS(create)(env, NULL, HRS_CODE_NRS, 10, 4));
+    CALL("create NRS", hn = NS(create)(env, NULL, HRS_CODE_NRS, 10, 4, 0));
     jobjectArray nin = rows(10, 65536, 23), nout = rows(4, 65536, 0);
     CALL("nrs encode", NS(encode)(env, NULL, hn, nin, nout, 65536));
     uint8_t* ni[10];
@@ -830,7 +919,7 @@ static int gpu_checks(void) {
     CALL("destroy NRS", NS(destroy)(env, NULL, hn));
 
     jlong hs = 0;
-    CALL("createSrc", hs = NS(createSrc)(env, NULL, 10, 6, 2));
+    CALL("createSrc", hs = NS(createSrc)(env, NULL, 10, 6, 2, 0));
     jobjectArray sin = rows(10, 40000, 25), sout = rows(6, 40000, 0);
     CALL("src encode", NS(encode)(env, NULL, hs, sin, sout, 40000));
     uint8_t* si[10];

@@ -155,3 +155,33 @@ def test_host_only_handle_refuses_coding():
 def test_geometry_accessors():
     code = HipReedSolomonCode(10, 4, device=NONE)
     assert (code.stripeSize(), code.paritySize(), code.symbolSize()) == (10, 4, 8)
+
+
+def test_scalar_decode5_host_logic_keeps_unlisted_values(monkeypatch):
+    """The mirror's scalar 5-arg decode (erasure_code.py) around its bulk call:
+    data zeroed at locationsNotToRead, and erasedValues[i] written only when
+    erasedLocations[i] is listed there (ReedSolomonCode.java:144-166). The bulk
+    call is stood in for by the oracle's decodeBulk here (no GPU); the GPU test
+    test_gpu_parity.py::test_scalar_decode5_leaves_unlisted_erased_values runs
+    the engine."""
+    import random
+    k, p = 10, 4
+    code = HipReedSolomonCode()
+    code._k, code._p = k, p
+
+    def bulk(rows, outs, erased, to_read, ntr):
+        got = C.decode_bulk5(k, p, [np.asarray(r) for r in rows], erased, to_read, ntr)
+        for o, g in zip(outs, got):
+            o[:] = g
+
+    monkeypatch.setattr(code, "decodeBulk", bulk)
+    rnd = random.Random(7)
+    for _ in range(30):
+        data = [rnd.randrange(256) for _ in range(k + p)]
+        ntr = sorted(rnd.sample(range(k + p), rnd.randrange(1, p + 1)))
+        erased = sorted(rnd.sample(range(k + p), rnd.randrange(1, p + 1)))
+        prefill = [rnd.randrange(256) for _ in erased]
+        want_vals, want_data = C.decode5(k, p, data, erased, [], ntr, values=prefill, with_data=True)
+        vals = list(prefill)
+        code.decode(data, erased, vals, [], ntr)
+        assert vals == want_vals and data == want_data

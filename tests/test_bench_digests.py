@@ -60,9 +60,13 @@ def test_combine_keys_for_runs_that_start_mid_block():
 def test_compare_rules():
     want = {"parity": {"0": "aa", "256": "bb", "9984+16": "ee"}, "decode": {"0": "cc"}}
     assert SD.compare({"parity": {"0": "aa"}, "decode": {"0": "cc"}}, want, ("parity", "decode"), 10_000) == \
-        {"blocks": 2, "match": True, "checked_stripes": 256, "unchecked_stripes": 0}
-    with pytest.raises(RuntimeError, match="cannot be checked"):  # a partial block inside the oracle's range
+        {"blocks": 2, "match": True, "checked_stripes": 256, "unchecked_stripes": 0, "partial_blocks": 0}
+    with pytest.raises(RuntimeError, match="no block"):  # only a partial block: nothing checkable
         SD.compare({"parity": {"0+128": "zz"}, "decode": {}}, want, ("parity", "decode"), 10_000)
+    # an ad-hoc run of 384 stripes: block 0 checked, the partial block 256+128 counted, not fatal
+    got = SD.compare({"parity": {"0": "aa", "256+128": "zz"}, "decode": {"0": "cc", "256+128": "yy"}}, want,
+                     ("parity", "decode"), 10_000)
+    assert got == {"blocks": 2, "match": True, "checked_stripes": 256, "unchecked_stripes": 128, "partial_blocks": 2}
     with pytest.raises(RuntimeError, match="!= oracle"):
         SD.compare({"parity": {"256": "xx"}, "decode": {}}, want, ("parity", "decode"), 10_000)
     with pytest.raises(RuntimeError, match="no block"):  # entirely outside the oracle's range

@@ -328,6 +328,32 @@ def test_scalar_encode_decode_like_TestErasureCodes(cuda):  # TestErasureCodes.j
             assert all(data[x] == 0 for x in erased)  # Java zeroes data[erased]
 
 
+def test_scalar_decode5_leaves_unlisted_erased_values(cuda):  # ReedSolomonCode.java:144-166
+    """An erased location missing from locationsNotToRead: the Java copies no
+    recovered value for it (:158-165), so erasedValues[i] keeps what the
+    caller passed; the listed ones are decoded; data is zeroed at
+    locationsNotToRead only. Compared with the oracle on pre-filled values."""
+    rnd = random.Random(29)
+    for k, p in [(10, 4), (6, 3), (3, 2), (12, 4)]:
+        code = HipReedSolomonCode(k, p)
+        n = k + p
+        for _ in range(12):
+            data = [rnd.randrange(256) for _ in range(n)]
+            ntr = sorted(rnd.sample(range(n), rnd.randrange(1, p + 1)))
+            outside = [x for x in range(n) if x not in ntr]
+            erased = sorted(rnd.sample(ntr, rnd.randrange(0, len(ntr) + 1)) + rnd.sample(outside, rnd.randrange(1, 3)))
+            prefill = [rnd.randrange(1, 256) for _ in erased]
+            to_read = [x for x in range(n) if x not in ntr]
+            want_vals, want_data = C.decode5(k, p, data, erased, to_read, ntr, values=prefill, with_data=True)
+            got_data, got_vals = list(data), list(prefill)
+            code.decode(got_data, erased, got_vals, to_read, ntr)
+            assert got_vals == want_vals, (k, p, erased, ntr)
+            assert got_data == want_data
+            for i, loc in enumerate(erased):
+                if loc not in ntr:
+                    assert got_vals[i] == prefill[i]
+
+
 def test_codec_registry_plugs_in_hip_code(cuda):
     conf = {codec_mod.ERASURE_CODING_CODECS_KEY: codec_mod.DEFAULT_CODECS_JSON,
             "hdfs.raid.erasure.code.rs": HipReedSolomonCode.JAVA_CLASS}

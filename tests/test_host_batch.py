@@ -21,15 +21,21 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine"])
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "duplex"])
 def transfer_mode(request, monkeypatch):
-    """Every test runs both ways the host batches can move bytes: zero copy (the
-    default: kernels read and write pinned host memory across the link) and
-    the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
-    if request.param == "copy_engine":
-        monkeypatch.setenv("HRS_ZEROCOPY", "0")
-    else:
+    """Every test runs every way the host batches can move bytes: zero copy
+    (the default: kernels read and write pinned host memory across the link),
+    the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H on each
+    slot's stream), and the copy engine with the directions split over the
+    shared copy-in / copy-out streams (HRS_HBATCH_DUPLEX=1: in_done /
+    comp_done / done events chain the three streams per slot)."""
+    monkeypatch.delenv("HRS_HBATCH_DUPLEX", raising=False)
+    if request.param == "zero_copy":
         monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    else:
+        monkeypatch.setenv("HRS_ZEROCOPY", "0")
+        if request.param == "duplex":
+            monkeypatch.setenv("HRS_HBATCH_DUPLEX", "1")
     return request.param
 
 

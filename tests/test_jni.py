@@ -61,3 +61,23 @@ def test_jni_bit_exact_on_gpu(cuda):
     rc, res = run("--gpu")
     assert rc == 0 and res["ok"], res
     assert res["jni_rule_violations"] == 0
+
+
+def test_java_codecs_take_a_device_from_the_conf():
+    """The Java drop-ins are Configurable (Codec.createErasureCode ->
+    ReflectionUtils.newInstance(class, conf), Codec.java:209-211) and create
+    their handle on HipDevices.pick(conf); HrsNative.create / createSrc carry
+    the device, as the shim's symbols do (the fake JVM calls them with explicit
+    ordinals, `--cpu` and `--gpu`). No JDK here: a source check."""
+    jdir = os.path.join(ROOT, "lambdafs_amd", "jni")
+    nat = open(os.path.join(jdir, "HrsNative.java")).read()
+    assert re.search(r"static native long create\(int code, int stripeSize, int paritySize, int device\)", nat)
+    assert re.search(r"static native long createSrc\([^)]*int device\)", nat)
+    assert "static native int deviceCount()" in nat
+    dev = open(os.path.join(jdir, "HipDevices.java")).read()
+    assert 'DEVICES_KEY = "hdfs.raid.hip.devices"' in dev
+    for cls in ("HipReedSolomonCode", "HipXORCode", "HipNativeReedSolomonCode", "HipSimpleRegeneratingCode"):
+        src = open(os.path.join(jdir, cls + ".java")).read()
+        assert f"public class {cls} extends ErasureCode implements Configurable" in src, cls
+        assert "public void setConf(Configuration conf)" in src and "HipDevices.pick(conf)" in src, cls
+        assert "HrsNative.create(" not in src.replace("return HrsNative.create(", ""), cls  # only via the wrapper

@@ -68,6 +68,28 @@ def test_c_and_python_decode_agree_on_non_codewords():
         assert [bytes(x) for x in c3] == py3
 
 
+def test_scalar_decode5_prefilled_values_agree():
+    """ReedSolomonCode.decode 5-arg (:144-166) with erased locations outside
+    locationsNotToRead: both transcriptions copy recovered values only for the
+    listed locations and leave the caller's other erasedValues untouched."""
+    rnd = random.Random(31)
+    for k, p in [(10, 4), (6, 3), (3, 2)]:
+        n = k + p
+        ref = R.ReedSolomonRef(k, p)
+        for _ in range(40):
+            data = [rnd.randrange(256) for _ in range(n)]
+            ntr = sorted(rnd.sample(range(n), rnd.randrange(1, p + 1)))
+            erased = sorted(rnd.sample(range(n), rnd.randrange(1, p + 1)))
+            prefill = [rnd.randrange(256) for _ in erased]
+            c_vals, c_data = C.decode5(k, p, data, erased, [], ntr, values=prefill, with_data=True)
+            py_data = list(data)
+            py_vals = ref.decode5(py_data, erased, [], ntr, values=prefill)
+            assert c_vals == py_vals and c_data == py_data
+            for i, loc in enumerate(erased):
+                if loc not in ntr:
+                    assert c_vals[i] == prefill[i]
+
+
 def test_bulk_remainder_zeroes_inputs_like_java():
     # GaloisField.java:326-338 runs in place: encodeBulk leaves its inputs zeroed.
     rows = [np.arange(8, dtype=np.uint8) + i for i in range(3)]

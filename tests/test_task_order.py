@@ -5,7 +5,11 @@ tasks than one block's waves, a last block with a short range, ranges that are n
 row tails (the byte-granular kernel) beside whole windows. Every streaming
 kernel family: static encode, fused encode + CRC, the pipelined and plain
 repairs, fused repair + CRC, the heterogeneous repair batch, CRC-32 windows.
-Bar: bit-exact (zlib for the CRCs)."""
+Bar: bit-exact. EVERY stripe is checked (a window an order misses or
+runs twice in the middle of the task range must not slip through): coded
+bytes against the byte-granular kernel (kernel mode 2, one byte column per
+lane, no window order at all) over the whole tensor plus the oracle on sampled
+stripes, CRCs against zlib for every cell."""
 import zlib
 
 import numpy as np
@@ -41,6 +45,16 @@ def _crc(b):
     return zlib.crc32(np.ascontiguousarray(b).tobytes()) & 0xFFFFFFFF
 
 
+def _bytewise(code, fn):
+    """fn() run on the byte-granular kernel (kernel mode 2: no windows, no
+    window order), the reference every stripe is compared with."""
+    code.setKernelMode(2)
+    try:
+        return fn()
+    finally:
+        code.setKernelMode(0)
+
+
 @pytest.mark.parametrize("S,L", SHAPES)
 def test_encode_and_encode_crc(cuda, order, S, L):
     torch = cuda
@@ -48,16 +62,20 @@ def test_encode_and_encode_crc(cuda, order, S, L):
     code = HipReedSolomonCode(k, p)
     st = _stripes(torch, S, k + p, L, seed=S + L)
     st[:, :p] = 0xA5
+    ref_dev = st.clone()
+    _bytewise(code, lambda: device.encode_stripes(code, ref_dev))
     device.encode_stripes(code, st)
     st2 = st.clone()
     st2[:, :p] = 0x5A
     crc = device.encode_stripes_crc(code, st2)
     torch.cuda.synchronize()
     host, host2, crcs = st.cpu().numpy(), st2.cpu().numpy(), crc.cpu().numpy().view(np.uint32)
+    assert np.array_equal(host, ref_dev.cpu().numpy()), (order, S, L)  # every stripe
     assert np.array_equal(host, host2)
     for s in _sample(S):
         ref = np.stack(C.encode_bulk(k, p, [host[s, p + c] for c in range(k)]))
         assert np.array_equal(host[s, :p], ref), (order, S, L, s)
+    for s in range(S):
         want = [_crc(host[s, p + c]) for c in range(k)] + [_crc(host[s, r]) for r in range(p)]
         assert list(crcs[s]) == want, (order, S, L, s)
 
@@ -76,16 +94,21 @@ def test_repairs(cuda, order, S, L, erased):
     device.decode_stripes(code, st, erased, ntr, out)
     out2 = torch.full_like(out, 0xA5)
     crc = device.decode_stripes_crc(code, st, erased, ntr, out2)
+    ref_dev = torch.full_like(out, 0x33)
+    _bytewise(code, lambda: device.decode_stripes(code, st, erased, ntr, ref_dev))
     torch.cuda.synchronize()
     host, got, got2 = st.cpu().numpy(), out.cpu().numpy(), out2.cpu().numpy()
     crcs = crc.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, ref_dev.cpu().numpy()), (order, S, L, erased)  # every stripe
     assert np.array_equal(got, got2)
     for s in _sample(S):
         reads = [host[s, i] if i in to_read else np.zeros(L, np.uint8) for i in range(n)]
         ref = C.decode_bulk5(k, p, reads, erased, to_read, ntr)
         for i in range(len(erased)):
             assert np.array_equal(got[s, i], ref[i]), (order, S, L, erased, s, i)
-            assert crcs[s, i] == _crc(ref[i])
+    for s in range(S):
+        for i in range(len(erased)):
+            assert crcs[s, i] == _crc(got[s, i]), (order, S, L, erased, s, i)
 
 
 @pytest.mark.parametrize("S,L", SHAPES)
@@ -119,5 +142,5 @@ def test_crc32_rows(cuda, order, S, L):
     crc = device.crc32_rows(code, [st[:, r] for r in range(3)])
     torch.cuda.synchronize()
     host, crcs = st.cpu().numpy(), crc.cpu().numpy().view(np.uint32)
-    for s in _sample(S):
+    for s in range(S):
         assert [int(x) for x in crcs[s]] == [_crc(host[s, r]) for r in range(3)], (order, S, L, s)
