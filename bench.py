@@ -71,7 +71,9 @@ def parse(argv=None):
     ap.add_argument("--p", type=int, default=4)
     ap.add_argument("--cpu-stripes", type=int, default=0,
                     help="stripes in the CPU baseline sample (0: 8 per thread)")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the config-5 end-to-end (host memory) leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the config-5 end-to-end (host memory) legs")
+    ap.add_argument("--e2e-devices", default="all",
+                    help="device set of the one-process config-5 leg (hdfs.raid.hip.devices syntax; world size 1)")
     ap.add_argument("--no-sha", action="store_true", help="skip the per-rank parity SHA-256")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-calls", action="store_true",
@@ -257,6 +259,86 @@ def host_calls(local, calls=100):
     return res
 
 
+def async_rounds(local, codecs=4, depths=(1, 2, 4), rounds=48):
+    """The asynchronous drop-in under Encoder-shaped traffic (VERDICT r4 item
+    5; HipReedSolomonCode.encodeBulkAsync / collect, Encoder.java:421-453):
+    `codecs` host threads, one codec each (raid.encoder.parallelism = 4
+    Encoders, Encoder.java:77-80), each keeping `depth` RS(10,4) rounds of one
+    1 MiB pageable stripe in flight (submit, and once `depth` are pending
+    collect the oldest). Per depth: the aggregate user-data rate, the wall
+    time of a round (submit to collected) and its GPU-side launch-to-completion
+    time (hrs_set_timing / hrs_ticket_gpu_ms, read after hrs_wait). The first
+    round of every codec is checked against the synchronous encode."""
+    import ctypes
+    import threading
+    from lambdafs_amd import _lib
+    from lambdafs_amd._lib import ptr_array
+    k, p, L = 10, 4, 1 << 20
+    lib = _lib.lib()
+    rng = np.random.default_rng(0x5EED000B)
+    workers = []
+    for c in range(codecs):
+        code = HipReedSolomonCode(k, p, device=local, zero_inputs_after_encode=False)
+        code._check(lib.hrs_set_timing(code._handle(), 1))
+        data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        ref = [np.zeros(L, np.uint8) for _ in range(p)]
+        code.encodeBulk(data, ref)
+        outs = [[np.zeros(L, np.uint8) for _ in range(p)] for _ in range(4)]
+        workers.append({"code": code, "h": code._handle(), "ins": ptr_array([d.ctypes.data for d in data]),
+                        "ref": ref, "outs": outs, "outp": [ptr_array([o.ctypes.data for o in ob]) for ob in outs]})
+    res = {"what": f"{codecs} threads x one RS(10,4) codec each, D rounds of one 1 MiB pageable stripe in flight "
+                   "per codec (hrs_encode_submit / hrs_wait / hrs_collect), one GPU", "rounds_per_codec": rounds}
+
+    def run_depth(depth):
+        errs, lat, gpu = [], [], []
+        lock = threading.Lock()
+
+        def body(w):
+            h, tq = w["h"], []
+            t = ctypes.c_uint64(0)
+            ms = ctypes.c_float(0)
+            my_lat, my_gpu = [], []
+            try:
+                for r in range(rounds + depth):
+                    if r < rounds:
+                        w["code"]._check(lib.hrs_encode_submit(h, w["ins"], L, 0, ctypes.byref(t)))
+                        tq.append((t.value, time.perf_counter(), r))
+                    if len(tq) == depth or (r >= rounds and tq):
+                        tk, t0, rr = tq.pop(0)
+                        w["code"]._check(lib.hrs_wait(h, tk))
+                        w["code"]._check(lib.hrs_ticket_gpu_ms(h, tk, ctypes.byref(ms)))
+                        slot = rr % 4
+                        w["code"]._check(lib.hrs_collect(h, tk, w["outp"][slot], None))
+                        my_lat.append((time.perf_counter() - t0) * 1e3)
+                        my_gpu.append(ms.value)
+                        if rr == 0 and not all(np.array_equal(a, b) for a, b in zip(w["outs"][slot], w["ref"])):
+                            raise RuntimeError("asynchronous encode differs from the synchronous one")
+            except Exception as e:  # noqa: BLE001 - reported after the join
+                errs.append(e)
+            with lock:
+                lat.extend(my_lat)
+                gpu.extend(my_gpu)
+
+        ths = [threading.Thread(target=body, args=(w,)) for w in workers]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        wall = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        return {"depth": depth, "wall_ms": round(wall * 1e3, 2),
+                "GiBps_user": round(codecs * rounds * k * L / GiB / wall, 2),
+                "round_wall_ms": {"median": round(float(np.median(lat)), 4), "p90": round(float(np.percentile(lat, 90)), 4)},
+                "round_gpu_ms": {"median": round(float(np.median(gpu)), 4), "p90": round(float(np.percentile(gpu, 90)), 4)}}
+
+    run_depth(1)  # warm every codec's slots and staging
+    res["by_depth"] = [run_depth(d) for d in depths]
+    res["bit_exact"] = True
+    return res
+
+
 def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     """BASELINE configs[4] end to end through the product's host batch API
     (hrs_decode_batch_host): RS(12,4), 256 KiB cells, S stripes per GPU (4,096
@@ -348,6 +430,78 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
         "stripes_per_gpu": S,
         "n_gpus": world,
     }
+
+
+def e2e_device_set(golden, spec, avail, per=512, L=256 << 10, reps=3):
+    """BASELINE configs[4] end to end through the drop-in's device set, in ONE
+    process: hrs_decode_batch_host_multi /
+    hrs_encode_batch_host_multi over one codec per device of `spec`
+    (hdfs.raid.hip.devices syntax, default every visible device): `per`
+    stripes per device, global stripes 0 .. per * members - 1 (4,096 on an
+    8-GPU node = config 5's total), pinned host memory, contiguous ranges, one
+    host thread per device. The repaired cells are checked against the
+    oracle's config-5 digests, the re-encoded parity against the device
+    encode. Runs at world size 1 only (one process drives every device)."""
+    from lambdafs_amd import devset
+    k, p = 12, 4
+    n = k + p
+    devs = devset.parse_device_set(spec, devset.device_count())
+    m = len(devs)
+    S = per * m
+    need = m * (per * (n + 2 + p) * L) + (2 << 30)  # pinned stripes + repaired cells + parity copy + process
+    if need > 0.75 * avail:
+        return {"skipped": f"device set {devs}: needs {need / GiB:.1f} GiB of host memory, "
+                           f"{avail / GiB:.1f} GiB available"}
+    st = torch.empty((S, n, L), dtype=torch.uint8, pin_memory=True)
+    gen = HipReedSolomonCode(k, p, device=devs[0])
+    chunk = torch.zeros((per, n, L), dtype=torch.uint8, device=f"cuda:{devs[0]}")
+    for g0 in range(0, S, per):  # synthetic stripes keyed by global index, parity from the device encode
+        synth.fill_data_rows(torch, chunk, 5, g0, k, p)
+        device.encode_stripes(gen, chunk)
+        st[g0:g0 + per].copy_(chunk)
+    del chunk
+    torch.cuda.synchronize()
+    par_ref = st[:, :p].clone()
+    stn = st.numpy()
+    er = np.array([np.sort(np.random.default_rng([0x5EED0005, g]).choice(n, 2, replace=False)) for g in range(S)],
+                  dtype=np.int32)
+    out = torch.zeros((S, 2, L), dtype=torch.uint8, pin_memory=True)
+    outn = out.numpy()
+    codes = [HipReedSolomonCode(k, p, device=d) for d in devs]
+
+    def timed(fn):
+        fn()
+        ms = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ms.append((time.perf_counter() - t0) * 1e3)
+        return ms
+
+    dec_ms = timed(lambda: device.decode_batch_host_multi(codes, stn, er, outn))
+    idx = np.arange(S)[:, None]
+    dec_ok = bool(np.array_equal(outn, stn[idx, er]))
+    repaired = SD.combine(SD.stripe_digests(lambda a, b: outn[a:b], S, 0))
+    st[:, :p] = 0
+    enc_ms = timed(lambda: device.encode_batch_host_multi(codes, stn))
+    enc_ok = bool(torch.equal(st[:, :p], par_ref))
+    user = k * L * S
+    t_dec, t_enc = float(np.median(dec_ms)), float(np.median(enc_ms))
+    res = {
+        "what": "configs[4] end to end through hrs_decode_batch_host_multi / hrs_encode_batch_host_multi: one "
+                f"process, one codec per device of {devs}, {per} stripes per device (global 0..{S - 1}), RS(12,4) "
+                "256 KiB cells, seeded random lost pair per stripe, pinned host memory, contiguous ranges, one host "
+                "thread per device",
+        "devices": devs, "members": m, "stripes": S,
+        "decode_ms": stats(dec_ms), "decode_GiBps_user": round(user / GiB / (t_dec * 1e-3), 3),
+        "decode_pcie_GBps_per_device": round((k + 2) * L * per / 1e9 / (t_dec * 1e-3), 2),
+        "encode_ms": stats(enc_ms), "encode_GiBps_user": round(user / GiB / (t_enc * 1e-3), 3),
+        "bit_exact": dec_ok and enc_ok,
+        "repaired_vs_oracle": SD.compare({"repaired": repaired}, golden.get("config5", {}), ("repaired",),
+                                         golden.get("config5", {}).get("stripes", 0)),
+    }
+    del st, out, par_ref
+    return res
 
 
 def gather_digests(mine):
@@ -507,7 +661,7 @@ def hbm_probes(dev, stripes=None, patterns=(), nbytes=4 << 30, reps=5):
                  "guide_copy_GBps": 6290.0,
                  "how": "4 GiB D2D (bytes read + written), hrs_probe_stream COPY over PROBE_SHAPES and torch "
                         "copy_; GBps = the fastest. guide_copy_GBps: MI355X_MICROARCH.md's float4 copy figure "
-                        "(box-to-box spread on this pool: DESIGN.md §5)"},
+                        "(box-to-box spread on this pool: profiles/r04/DESIGN_history.md §5)"},
         "read_GBps": reads[best(reads)], "read_best": best(reads),
         "write_GBps": writes[best(writes)], "write_best": best(writes),
         "read_variants": reads, "write_variants": writes,
@@ -791,6 +945,12 @@ def run(args):
             e2e["memory_guard"] = e2e_why
         if not e2e["bit_exact"]:
             raise RuntimeError("config 5 end-to-end leg: outputs differ from the device-resident ones")
+    e2e_set = None
+    if world == 1 and not args.no_e2e:  # one process over the device set (hrs_*_batch_host_multi)
+        torch.cuda.empty_cache()
+        e2e_set = e2e_device_set(golden, args.e2e_devices, host_available_bytes())
+        if e2e_set.get("bit_exact") is False:
+            raise RuntimeError("config 5 device-set leg: outputs differ from the device-resident ones")
 
     total_stripes = args.stripes if args.strong else S * world
     user_bytes = 2 * k * L * total_stripes * args.steps
@@ -900,9 +1060,11 @@ def run(args):
             "hbm_probes": probes,
             "parity_sha256": sha,
             "e2e_config5": e2e,
+            "e2e_device_set": e2e_set,
             "cpu_baseline": None,
         }
         res["host_calls"] = None if args.no_host_calls else host_calls(local)
+        res["async_rounds"] = None if args.no_host_calls else async_rounds(local)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
             res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 40, threads=1)

@@ -249,6 +249,15 @@ hrs_status hrs_wait(hrs_codec* codec, uint64_t ticket);
 hrs_status hrs_release(hrs_codec* codec, uint64_t ticket);
 /* Uncollected operations of this handle. */
 int hrs_pending(const hrs_codec* codec);
+/* Diagnostic: with timing on (hrs_set_timing(codec, 1); off by default), each
+ * submitted operation records a timing event before its first GPU operation
+ * and one after its last, on its slot's stream; hrs_ticket_gpu_ms then gives
+ * the GPU-side launch-to-completion time of a waited-for (hrs_wait) and not
+ * yet collected operation. HRS_EINVAL for an unknown ticket or an operation
+ * submitted with timing off. Lets a benchmark put the GPU time of small
+ * asynchronous rounds beside their wall time. */
+hrs_status hrs_set_timing(hrs_codec* codec, int on);
+hrs_status hrs_ticket_gpu_ms(const hrs_codec* codec, uint64_t ticket, float* ms);
 /* Shape of an uncollected operation: output rows, their length, CRC values
  * (0 if not checksummed). HRS_EINVAL for an unknown ticket. */
 hrs_status hrs_ticket_shape(const hrs_codec* codec, uint64_t ticket, int* num_outputs, size_t* len, int* num_crcs);

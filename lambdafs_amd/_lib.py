@@ -42,6 +42,7 @@ EXPORTS = (
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
     "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_wait", "hrs_release",
     "hrs_device_count", "hrs_codec_device", "hrs_decode_batch_host_multi", "hrs_encode_batch_host_multi",
+    "hrs_set_timing", "hrs_ticket_gpu_ms",
 )
 # include/hrs_probe.h, exported by libhrs_probe.so
 PROBE_EXPORTS = ("hrs_probe_stream", "hrs_probe_rows")
@@ -108,6 +109,8 @@ def lib():
         "hrs_decode_batch_host_multi": ([PP, I, P, S, S, P, I, P, S, S, S, S], I),
         "hrs_encode_batch_host_multi": ([PP, I, P, S, S, S, S], I),
         "hrs_device_count": ([], I),
+        "hrs_set_timing": ([P, I], I),
+        "hrs_ticket_gpu_ms": ([P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float)], I),
         "hrs_codec_device": ([P], I),
         "hrs_encode_submit": ([P, PP, S, I, ctypes.POINTER(ctypes.c_uint64)], I),
         "hrs_decode_submit": ([P, PP, IP, I, IP, I, IP, I, S, I, ctypes.POINTER(ctypes.c_uint64)], I),

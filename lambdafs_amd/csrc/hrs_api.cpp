@@ -187,7 +187,8 @@ void hrs_destroy(hrs_codec* c) {
       (void)hipStreamSynchronize(a.stream);
       (void)hipStreamDestroy(a.stream);
     }
-    if (a.done) (void)hipEventDestroy(a.done);
+    for (hipEvent_t e : {a.done, a.t_start, a.t_end})
+      if (e) (void)hipEventDestroy(e);
     if (a.dev) (void)hipFree(a.dev);
     if (a.pin) (void)hipHostFree(a.pin);
   }

@@ -62,8 +62,9 @@ struct hrs_codec {
     bool pending = false;
   } batch[2];
   int batch_next = 0;
-  // host-buffer calls: two chunk slots, each pinned staging + device rows +
-  // its own stream; a slot is reused once its D2H event has completed
+  // host-buffer calls: chunk slots (2 by default, HRS_HOST_SLOTS up to 4),
+  // each pinned staging + device rows + its own stream; a slot is reused once
+  // its D2H event has completed
   struct HostSlot {
     uint8_t* pin = nullptr;
     uint8_t* pin_dev = nullptr;  // device address of `pin` (zero-copy kernels)
@@ -71,7 +72,7 @@ struct hrs_codec {
     size_t bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-  } host[2];
+  } host[hrs::kHostSlots];
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
   // its own compute stream; every slot's H2D goes on one copy-in stream and
@@ -101,6 +102,9 @@ struct hrs_codec {
     size_t bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    hipEvent_t t_start = nullptr;  // timing events (hrs_set_timing)
+    hipEvent_t t_end = nullptr;
+    bool timed = false;   // this operation recorded t_start / t_end
     bool busy = false;
     bool queued = false;  // GPU work was queued (len > 0)
     uint64_t ticket = 0;
@@ -108,6 +112,7 @@ struct hrs_codec {
     size_t len = 0, pitch = 0, crc_off = 0;
   } async[hrs::kAsyncSlots];
   uint64_t async_tickets = 0;
+  bool timing = false;  // hrs_set_timing: asynchronous operations record timing events
   std::string err;
   std::string last_kernel;  // main kernel of the latest coding call (hrs_last_kernel)
 };

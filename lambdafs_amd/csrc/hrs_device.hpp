@@ -399,7 +399,7 @@ __device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* tree, uint32_t
 // nin x 2 KiB in flight; coefficients are wave-uniform kernel arguments.
 // Bit loop unrolled (xtime is then a free relabel of the planes) unless the
 // body would outgrow the instruction cache: unrolled, bitsliced<4,12> is
-// 28 KiB of branchy code and ran 40% slower than rolled.
+// 28 KiB of branchy code and ran 40% slower than rolled (profiles/r04/DESIGN_history.md §3).
 template <int NOUT, int NINB>
 struct BitLoop {
   static constexpr bool kRolled = NOUT * NINB >= 40;

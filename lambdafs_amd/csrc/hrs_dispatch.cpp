@@ -410,7 +410,7 @@ hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strid
 
 // Slicing-table copies the fused kernel's lanes spread over: 32 (each lane of
 // a 32-lane group on its own LDS bank); HRS_CRC_REP = 16 | 8 | 4 | 2 | 1 reads
-// fewer copies (A/B of the replication factor; read per call).
+// fewer copies (A/B of the replication factor, profiles/r03/ab/NOTES.md; read per call).
 uint32_t crc_rep_mask() {
   const char* e = getenv("HRS_CRC_REP");
   const int r = e ? atoi(e) : hrs::kCrcRep;

@@ -25,15 +25,27 @@ size_t pitch_for(size_t len) { return (len + 255) & ~static_cast<size_t>(255); }
 
 // Host rows -> device, apply m, device -> host rows; synchronous. The rows
 // (pageable: a JNI-pinned Java array) go through pinned staging in column
-// chunks over two slots: while the copy pool moves chunk j into one slot's
-// staging (and chunk j-2's outputs out of it), the GPU runs chunk j-1's H2D,
-// kernel and D2H on the other slot's stream.
+// chunks over a ring of slots (2 by default): while the copy pool moves chunk
+// j into one slot's staging (and chunk j - nslots's outputs out of it), the GPU
+// runs the previous chunks' H2D, kernel and D2H on the other slots' streams.
 size_t host_chunk_bytes() {
   static const size_t v = [] {
     const char* e = getenv("HRS_HOST_CHUNK");
     long x = e ? atol(e) : 0;
     if (x < static_cast<long>(hrs::kWindowBytes)) x = 512 << 10;  // measured best (tools/host_sweep.sh)
     return static_cast<size_t>(x) / hrs::kWindowBytes * hrs::kWindowBytes;
+  }();
+  return v;
+}
+
+// Chunk slots a call rotates through: 2 (the default) or up to kHostSlots,
+// so the copy of chunk j need not wait for chunk j - 2's kernel (HRS_HOST_SLOTS,
+// read once).
+int host_slots() {
+  static const int v = [] {
+    const char* e = getenv("HRS_HOST_SLOTS");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 2 && x <= hrs::kHostSlots) ? x : 2;
   }();
   return v;
 }
@@ -111,7 +123,8 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
   const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
   const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
   const size_t need = ncrc ? raw_off + crc_raw_bytes_for(chunk, 1, ncrc) : crc_off;
-  for (int i = 0; i < 2; ++i) {
+  const int nslots = host_slots();
+  for (int i = 0; i < nslots; ++i) {
     hrs_status st = host_slot(c, i, need);
     if (st != HRS_OK) return st;
   }
@@ -121,8 +134,9 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
   // kernel takes it (a two-pass CRC would read the cells across the link a
   // second time); other chunks take the copy engine. The raw window CRCs stay
   // in device memory.
-  uint8_t* const zpin[2] = {c->host[0].pin_dev, c->host[1].pin_dev};
-  const bool zc_ok = zero_copy_on() && zpin[0] && zpin[1];
+  uint8_t* zpin[hrs::kHostSlots] = {};
+  bool zc_ok = zero_copy_on();
+  for (int i = 0; i < nslots; ++i) zc_ok &= (zpin[i] = c->host[i].pin_dev) != nullptr;
   auto zc_chunk = [&](size_t lj) {
     if (!zc_ok) return false;
     if (crc.mode == kCrcEncode) return encode_crc_one_pass(c, lj, 1);
@@ -131,8 +145,8 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
   };
   hrs::CopyPool& pool = hrs::CopyPool::instance();
   std::vector<hrs::CopyJob> jobs;
-  size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
-  bool pending[2] = {false, false};
+  size_t pend_off[hrs::kHostSlots] = {}, pend_len[hrs::kHostSlots] = {};
+  bool pending[hrs::kHostSlots] = {};
   auto finish = [&](int sl) -> hrs_status {  // wait for a slot, copy its outputs out
     if (!pending[sl]) return HRS_OK;
     hipError_t e = hipEventSynchronize(c->host[sl].done);
@@ -152,7 +166,7 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
   std::vector<const uint8_t*> din(nin);
   std::vector<uint8_t*> dout(nout);
   for (size_t j = 0; j < nchunks; ++j) {
-    const int sl = static_cast<int>(j & 1);
+    const int sl = static_cast<int>(j % nslots);
     hrs_codec::HostSlot& h = c->host[sl];
     hrs_status st = finish(sl);
     if (st != HRS_OK) return st;
@@ -194,8 +208,8 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     pend_off[sl] = off;
     pend_len[sl] = lj;
   }
-  for (size_t j = nchunks > 2 ? nchunks - 2 : 0; j < nchunks; ++j) {
-    hrs_status st = finish(static_cast<int>(j & 1));
+  for (size_t j = nchunks > static_cast<size_t>(nslots) ? nchunks - nslots : 0; j < nchunks; ++j) {
+    hrs_status st = finish(static_cast<int>(j % nslots));
     if (st != HRS_OK) return st;
   }
   return HRS_OK;
@@ -275,6 +289,17 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
                    : crc_mode == kCrcOutputs ? apply_crc_one_pass(c, nout, nlive, len)
                                              : true);
   hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
+  a.timed = false;
+  if (c->timing) {
+    for (hipEvent_t* ev : {&a.t_start, &a.t_end})
+      if (!*ev) {
+        hipError_t e = hipEventCreate(ev);
+        if (e != hipSuccess) return hip_fail(c, e, "hipEventCreate");
+      }
+    hipError_t e = hipEventRecord(a.t_start, a.stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+    a.timed = true;
+  }
   if (nlive > 0 && !zc) {
     hipError_t e = hipMemcpyAsync(a.dev, a.pin, pitch * (nlive - 1) + len, hipMemcpyHostToDevice, a.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
@@ -299,6 +324,7 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
     e = hipMemcpyAsync(a.pin + pitch * nlive, a.dev + pitch * nlive, back, hipMemcpyDeviceToHost, a.stream);
     if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
   }
+  if (a.timed && (e = hipEventRecord(a.t_end, a.stream)) != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   e = hipEventRecord(a.done, a.stream);
   if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   a.nout = nout;
@@ -324,6 +350,7 @@ hrs_status async_submit(hrs_codec* c, const uint8_t* m, int nout, int nin, const
   hrs_codec::AsyncSlot& a = c->async[free_slot];
   const int ncrc = crc_mode == kCrcEncode ? nin + nout : crc_mode == kCrcOutputs ? nout : 0;
   a.queued = false;
+  a.timed = false;
   a.nout = nout;
   a.ncrc = ncrc;
   a.len = len;
@@ -526,6 +553,26 @@ hrs_status hrs_ticket_shape(const hrs_codec* c, uint64_t ticket, int* num_output
       return HRS_OK;
     }
   return HRS_EINVAL;
+}
+
+hrs_status hrs_set_timing(hrs_codec* c, int on) {
+  if (!c) return HRS_EINVAL;
+  c->timing = on != 0;
+  return HRS_OK;
+}
+
+hrs_status hrs_ticket_gpu_ms(const hrs_codec* cc, uint64_t ticket, float* ms) {
+  auto* c = const_cast<hrs_codec*>(cc);
+  if (!c || !ms) return HRS_EINVAL;
+  for (auto& s : c->async)
+    if (s.busy && s.ticket == ticket) {
+      if (!s.queued || !s.timed) return fail(c, HRS_EINVAL, "operation %llu was submitted without timing",
+                                             static_cast<unsigned long long>(ticket));
+      DeviceGuard g(c->device);
+      const hipError_t e = hipEventElapsedTime(ms, s.t_start, s.t_end);
+      return e == hipSuccess ? HRS_OK : hip_fail(c, e, "hipEventElapsedTime");
+    }
+  return fail(c, HRS_EINVAL, "no uncollected operation with ticket %llu", static_cast<unsigned long long>(ticket));
 }
 
 int hrs_pending(const hrs_codec* c) {

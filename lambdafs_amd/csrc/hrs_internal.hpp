@@ -71,6 +71,7 @@ const char* last_kernel();
 constexpr int kBatchMaxIn = 32;  // > 16 inputs (or > 8 with 6-8 outputs): batch_stream_kernel
 constexpr int kHostBatchSlots = 3;  // chunk slots of the host-memory batch pipeline
 constexpr int kAsyncSlots = 4;      // operations in flight per handle (hrs_*_submit / hrs_collect)
+constexpr int kHostSlots = 4;       // chunk slots of a synchronous host-buffer call (at most; HRS_HOST_SLOTS)
 struct BatchPlan {            // one erasure pattern, a device table entry
   int nin;                    // live survivor rows read
   int nout;                   // erased rows written
