@@ -22,13 +22,17 @@ JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
             tests/cpp/copy_pool_test
 
-TOOLS    := tools/host_call_rate
+TOOLS    := tools/host_call_rate tools/register_zc_probe
 
 all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
 
 # The synchronous C-ABI call rate (bench.py's host_calls leg, profiles/r05/).
 tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
+
+# Staged vs page-registered synchronous calls (profiles/r05/NOTES.md).
+tools/register_zc_probe: tools/register_zc_probe.cpp include/hrs.h $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build

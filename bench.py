@@ -284,7 +284,8 @@ def async_rounds(local, codecs=4, depths=(1, 2, 4), rounds=48):
         ref = [np.zeros(L, np.uint8) for _ in range(p)]
         code.encodeBulk(data, ref)
         outs = [[np.zeros(L, np.uint8) for _ in range(p)] for _ in range(4)]
-        workers.append({"code": code, "h": code._handle(), "ins": ptr_array([d.ctypes.data for d in data]),
+        workers.append({"code": code, "h": code._handle(), "data": data,  # data: keeps the rows `ins` points at alive
+                        "ins": ptr_array([d.ctypes.data for d in data]),
                         "ref": ref, "outs": outs, "outp": [ptr_array([o.ctypes.data for o in ob]) for ob in outs]})
     res = {"what": f"{codecs} threads x one RS(10,4) codec each, D rounds of one 1 MiB pageable stripe in flight "
                    "per codec (hrs_encode_submit / hrs_wait / hrs_collect), one GPU", "rounds_per_codec": rounds}

@@ -42,7 +42,7 @@ EXPORTS = (
     "hrs_encode_submit", "hrs_decode_submit", "hrs_collect", "hrs_pending", "hrs_ticket_shape",
     "hrs_set_kernel_mode", "hrs_last_kernel", "hrs_wait", "hrs_release",
     "hrs_device_count", "hrs_codec_device", "hrs_decode_batch_host_multi", "hrs_encode_batch_host_multi",
-    "hrs_set_timing", "hrs_ticket_gpu_ms",
+    "hrs_set_timing", "hrs_ticket_gpu_ms", "hrs_last_host_path",
 )
 # include/hrs_probe.h, exported by libhrs_probe.so
 PROBE_EXPORTS = ("hrs_probe_stream", "hrs_probe_rows")
@@ -121,6 +121,7 @@ def lib():
         "hrs_ticket_shape": ([P, ctypes.c_uint64, IP, ctypes.POINTER(ctypes.c_size_t), IP], I),
         "hrs_set_kernel_mode": ([P, I], I),
         "hrs_last_kernel": ([P], ctypes.c_char_p),
+        "hrs_last_host_path": ([P], ctypes.c_char_p),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -182,6 +182,8 @@ void hrs_destroy(hrs_codec* c) {
     if (h.dev) (void)hipFree(h.dev);
     if (h.pin) (void)hipHostFree(h.pin);
   }
+  if (c->direct_crc) (void)hipHostFree(c->direct_crc);
+  if (c->direct_raw) (void)hipFree(c->direct_raw);
   for (auto& a : c->async) {
     if (a.stream) {
       (void)hipStreamSynchronize(a.stream);
@@ -220,6 +222,8 @@ void hrs_destroy(hrs_codec* c) {
 const char* hrs_last_error(const hrs_codec* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
 
 const char* hrs_last_kernel(const hrs_codec* c) { return c ? c->last_kernel.c_str() : ""; }
+
+const char* hrs_last_host_path(const hrs_codec* c) { return c ? c->last_host_path : ""; }
 
 int hrs_device_count(void) {
   int n = 0;

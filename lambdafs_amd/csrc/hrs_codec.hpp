@@ -73,6 +73,13 @@ struct hrs_codec {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
   } host[hrs::kHostSlots];
+  // synchronous calls run straight over the caller's rows (pages registered
+  // for the call, hrs_hostpath.cpp host_apply_direct): the call's CRC words
+  // (pinned, device-mapped) and its raw window-CRC scratch (device)
+  uint32_t* direct_crc = nullptr;
+  uint32_t* direct_crc_dev = nullptr;
+  uint32_t* direct_raw = nullptr;
+  size_t direct_raw_bytes = 0;
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
   // its own compute stream; every slot's H2D goes on one copy-in stream and
@@ -115,6 +122,7 @@ struct hrs_codec {
   bool timing = false;  // hrs_set_timing: asynchronous operations record timing events
   std::string err;
   std::string last_kernel;  // main kernel of the latest coding call (hrs_last_kernel)
+  const char* last_host_path = "";  // hrs_last_host_path: "direct" | "staged" | "copy_engine"
 };
 
 

@@ -95,6 +95,130 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
   return it->second;
 }
 
+// ---- synchronous calls straight over the caller's rows (round 5) ----
+// The staged path copies the caller's pageable rows into pinned staging and
+// the outputs back (a 1 MiB-cell RS(10,4) call: 10 MiB in, 4 MiB out, the
+// first copy-in and the last copy-out on the critical path). Instead, the
+// pages under the call's rows are registered with HIP for the duration of the
+// call (hipHostRegister, mapped: ~0.6 us per row) and the zero-copy kernel
+// reads the inputs and writes the outputs across the host link in place; the
+// pages are unregistered once the kernel has completed. tools/register_zc_probe.cpp,
+// one process, interleaved (profiles/r05/NOTES.md): encode 0.262 ms vs 0.325
+// staged, decode 0.239 vs 0.268. Taken when zero copy is on, every row is
+// 16-byte aligned (the vector kernels; a JVM places a 1 MiB byte[]'s data 16
+// bytes past a G1 region start), len >= HRS_HOST_DIRECT_MIN (64 KiB: below it
+// the copies cost less than the registrations), a checksummed call's kernel
+// is one-pass (a two-pass CRC would read the cells across the link twice),
+// and every range registers (pages another call or the caller already
+// registered fail it: the call then takes the staged path, same results).
+// HRS_HOST_DIRECT=0 turns it off (A/B runs and the staged-path tests; read per call).
+bool host_direct_on() {
+  const char* e = getenv("HRS_HOST_DIRECT");
+  return !(e && e[0] == '0');
+}
+
+size_t host_direct_min() {
+  static const size_t v = [] {
+    const char* e = getenv("HRS_HOST_DIRECT_MIN");
+    const long x = e ? atol(e) : -1;
+    return x >= 0 ? static_cast<size_t>(x) : static_cast<size_t>(64) << 10;
+  }();
+  return v;
+}
+
+// Runs the call over the caller's rows; false (nothing done, nothing left
+// registered) when the call must take the staged path. *st: its status.
+bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
+                       uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc, int nlive,
+                       hrs_status* st) {
+  if (!host_direct_on() || !zero_copy_on() || len < host_direct_min()) return false;
+  if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, len, 1)) return false;
+  if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, len)) return false;
+  constexpr uintptr_t kPage = 4096;
+  std::vector<std::pair<uintptr_t, uintptr_t>> rg;
+  auto add = [&](const void* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    rg.push_back({a & ~(kPage - 1), (a + len + kPage - 1) & ~(kPage - 1)});
+    return aligned16(p);
+  };
+  for (int i = 0; i < nin; ++i)
+    if (din[i] && !add(din[i])) return false;
+  for (int o = 0; o < nout; ++o)
+    if (!add(out_rows[o])) return false;
+  std::sort(rg.begin(), rg.end());
+  size_t w = 0;  // merge ranges that share pages (rows of one heap region)
+  for (size_t r = 1; r < rg.size(); ++r) {
+    if (rg[r].first < rg[w].second)
+      rg[w].second = std::max(rg[w].second, rg[r].second);
+    else
+      rg[++w] = rg[r];
+  }
+  rg.resize(rg.empty() ? 0 : w + 1);
+  // the stream and, for checksums, the CRC words and scratch, before any page is registered
+  hrs_status s0 = host_slot(c, 0, 0);
+  if (s0 == HRS_OK && ncrc > 0 && !c->direct_crc) {
+    hipError_t e = hipHostMalloc(&c->direct_crc, 1024 * sizeof(uint32_t), hipHostMallocDefault);
+    if (e != hipSuccess) s0 = fail(c, HRS_ENOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+    uint8_t* d = nullptr;
+    if (s0 == HRS_OK && host_device_ptr(c->direct_crc, &d)) c->direct_crc_dev = reinterpret_cast<uint32_t*>(d);
+  }
+  if (s0 == HRS_OK && ncrc > 0 && !c->direct_crc_dev) return false;
+  const size_t raw_need = ncrc > 0 ? crc_raw_bytes_for(len, 1, ncrc) : 0;
+  if (s0 == HRS_OK && raw_need > c->direct_raw_bytes) {
+    if (c->direct_raw) (void)hipFree(c->direct_raw);  // no call of this handle is in flight
+    c->direct_raw = nullptr;
+    c->direct_raw_bytes = 0;
+    hipError_t e = hipMalloc(&c->direct_raw, raw_need);
+    if (e != hipSuccess) s0 = fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", raw_need, hipGetErrorString(e));
+    else c->direct_raw_bytes = raw_need;
+  }
+  if (s0 != HRS_OK) {
+    *st = s0;
+    return true;
+  }
+  std::vector<uintptr_t> held;
+  auto release = [&] {
+    for (uintptr_t a : held) (void)hipHostUnregister(reinterpret_cast<void*>(a));
+  };
+  for (const auto& r : rg) {
+    if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first, hipHostRegisterMapped) != hipSuccess) {
+      (void)hipGetLastError();  // already registered (by the caller or another call), or not registrable
+      release();
+      return false;
+    }
+    held.push_back(r.first);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(r.first), 0) != hipSuccess ||
+        d != reinterpret_cast<void*>(r.first)) {  // zero copy needs the device address to be the host address
+      (void)hipGetLastError();
+      release();
+      return false;
+    }
+  }
+  const hipStream_t s = c->host[0].stream;
+  c->last_host_path = "direct";
+  hrs_status rs;
+  {
+    hrs::GridCap cap(zero_copy_blocks());
+    if (crc.mode == kCrcEncode)
+      rs = encode_crc_impl(c, din, 0, out_rows, 0, len, 1, nullptr, c->direct_crc_dev, s, c->direct_raw);
+    else if (crc.mode == kCrcOutputs)
+      rs = apply_crc_impl(c, m, nout, nin, din, 0, out_rows, 0, len, 1, nullptr, c->direct_crc_dev, s, c->direct_raw);
+    else
+      rs = run_apply(c, m, nout, nin, din, 0, out_rows, 0, len, 1, s, static_kp);
+  }
+  // whatever the launch did, nothing may touch the pages once they are unregistered
+  const hipError_t e = hipStreamSynchronize(s);
+  if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
+  release();
+  if (rs == HRS_OK && ncrc > 0) {  // CRC32.update chaining: crc = Z_len(crc) ^ crc(cell)
+    const hrs::crc::Mat& z = crc_zmat(c, len);
+    for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ c->direct_crc[r];
+  }
+  *st = rs;
+  return true;
+}
+
 hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                            uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc) {
   const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
@@ -115,6 +239,12 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
   }
   for (int o = 0; o < nout; ++o)
     if (!out_rows[o]) return fail(c, HRS_EINVAL, "output row %d is NULL", o);
+  {
+    std::vector<const uint8_t*> live_rows(nin);
+    for (int i = 0; i < nin; ++i) live_rows[i] = slot_of[i] >= 0 ? in_rows[i] : nullptr;
+    hrs_status st = HRS_OK;
+    if (host_apply_direct(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, nlive, &st)) return st;
+  }
   const size_t chunk = std::min(len, host_chunk_bytes());
   const size_t pitch = pitch_for(chunk);
   const size_t nchunks = (len + chunk - 1) / chunk;
@@ -176,6 +306,7 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
       if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
     pool.run(jobs);
     const bool zc = zc_chunk(lj);
+    c->last_host_path = zc ? "staged" : "copy_engine";
     // only zero-copy chunks cap their grid (the link bounds them); a chunk
     // sent back to the copy engine runs on device memory with the full grid
     hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);

@@ -256,6 +256,11 @@ class _HipErasureCode(ErasureCode):
         it (hrs_last_kernel); "" before any device work."""
         return _lib.lib().hrs_last_kernel(self._handle()).decode()
 
+    def lastHostPath(self):
+        """How the latest synchronous host-buffer call moved its bytes
+        (hrs_last_host_path): "direct", "staged", "copy_engine" or ""."""
+        return _lib.lib().hrs_last_host_path(self._handle()).decode()
+
     def encodeMatrix(self):
         g = np.zeros((self._p, self._k), dtype=np.uint8)
         self._check(_lib.lib().hrs_encode_matrix(self._handle(), g.ctypes.data))

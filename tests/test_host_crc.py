@@ -24,16 +24,20 @@ def test_host_crc_exported():
     assert hasattr(L, "hrs_encode_crc") and hasattr(L, "hrs_decode_crc")
 
 
-@pytest.fixture(params=["zero_copy", "copy_engine"])
+@pytest.fixture(params=["direct", "zero_copy", "copy_engine"])
 def transfer_mode(request, monkeypatch):
-    """The GPU tests run both ways the checksummed host-buffer calls can move
-    bytes: zero copy (the default where the one-pass kernel takes the chunk:
-    kernels read and write the pinned staging, CRCs included) and the copy
-    engine (HRS_ZEROCOPY=0)."""
-    if request.param == "copy_engine":
+    """Every test runs each way the synchronous host-buffer calls can move
+    bytes: straight over the caller's rows (the default where they qualify:
+    their pages registered for the call, the zero-copy kernel reads and writes
+    them in place), the staged zero-copy path (HRS_HOST_DIRECT=0: rows copied
+    into pinned staging, the kernel works on the staging) and the copy engine
+    (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
+    monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
+    monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    if request.param == "zero_copy":
+        monkeypatch.setenv("HRS_HOST_DIRECT", "0")
+    elif request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
-    else:
-        monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
     return request.param
 
 

@@ -11,15 +11,20 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine"])
+@pytest.fixture(autouse=True, params=["direct", "zero_copy", "copy_engine"])
 def transfer_mode(request, monkeypatch):
-    """Every test runs both ways the synchronous calls can move bytes: zero copy (the
-    default: kernels read and write pinned host memory across the link) and
-    the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
-    if request.param == "copy_engine":
+    """Every test runs each way the synchronous host-buffer calls can move
+    bytes: straight over the caller's rows (the default where they qualify:
+    their pages registered for the call, the zero-copy kernel reads and writes
+    them in place), the staged zero-copy path (HRS_HOST_DIRECT=0: rows copied
+    into pinned staging, the kernel works on the staging) and the copy engine
+    (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
+    monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
+    monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    if request.param == "zero_copy":
+        monkeypatch.setenv("HRS_HOST_DIRECT", "0")
+    elif request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
-    else:
-        monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
     return request.param
 
 
