@@ -97,6 +97,8 @@ class HipCode : public ErasureCode {
   int paritySize() const override { return hrs_parity_size(h_); }
   int symbolSize() const override { return hrs_symbol_size(h_); }
   hrs_codec* handle() const { return h_; }
+  // the GPU this codec runs on (hrs_codec_device; hrs_opts.device at creation)
+  int device() const { return hrs_codec_device(h_); }
 
   // the product's list (hrs_locations_to_read_list): SRC returns a local group
   std::vector<int> locationsToReadForDecode(const std::vector<int>& erasedLocations) const override {
@@ -212,6 +214,29 @@ class HipCode : public ErasureCode {
  protected:
   hrs_codec* h_ = nullptr;
 };
+
+// Host batches over a device set (hrs_encode_batch_host_multi /
+// hrs_decode_batch_host_multi): one codec per device, equal contiguous stripe
+// ranges, one host thread each. Layout and semantics as the single-codec
+// calls (include/hrs.h).
+inline void encodeBatchHostMulti(const std::vector<HipCode*>& codes, uint8_t* stripes, size_t rowStride,
+                                 size_t stripeStride, size_t len, size_t nstripes) {
+  std::vector<hrs_codec*> h;
+  for (HipCode* c : codes) h.push_back(c->handle());
+  check(hrs_encode_batch_host_multi(h.data(), static_cast<int>(h.size()), stripes, rowStride, stripeStride, len,
+                                    nstripes),
+        h.empty() ? nullptr : h[0]);
+}
+
+inline void decodeBatchHostMulti(const std::vector<HipCode*>& codes, const uint8_t* stripes, size_t rowStride,
+                                 size_t stripeStride, const int* erased, int maxErased, uint8_t* out,
+                                 size_t outRowStride, size_t outStripeStride, size_t len, size_t nstripes) {
+  std::vector<hrs_codec*> h;
+  for (HipCode* c : codes) h.push_back(c->handle());
+  check(hrs_decode_batch_host_multi(h.data(), static_cast<int>(h.size()), stripes, rowStride, stripeStride, erased,
+                                    maxErased, out, outRowStride, outStripeStride, len, nstripes),
+        h.empty() ? nullptr : h[0]);
+}
 
 class HipReedSolomonCode : public HipCode {
  public:

@@ -182,7 +182,6 @@ void hrs_destroy(hrs_codec* c) {
     if (h.dev) (void)hipFree(h.dev);
     if (h.pin) (void)hipHostFree(h.pin);
   }
-  if (c->direct_crc) (void)hipHostFree(c->direct_crc);
   if (c->direct_raw) (void)hipFree(c->direct_raw);
   for (auto& a : c->async) {
     if (a.stream) {

@@ -74,10 +74,7 @@ struct hrs_codec {
     hipEvent_t done = nullptr;
   } host[hrs::kHostSlots];
   // synchronous calls run straight over the caller's rows (pages registered
-  // for the call, hrs_hostpath.cpp host_apply_direct): the call's CRC words
-  // (pinned, device-mapped) and its raw window-CRC scratch (device)
-  uint32_t* direct_crc = nullptr;
-  uint32_t* direct_crc_dev = nullptr;
+  // for the call, hrs_hostpath.cpp host_apply_direct): raw window-CRC scratch
   uint32_t* direct_raw = nullptr;
   size_t direct_raw_bytes = 0;
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -99,19 +100,31 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
 // The staged path copies the caller's pageable rows into pinned staging and
 // the outputs back (a 1 MiB-cell RS(10,4) call: 10 MiB in, 4 MiB out, the
 // first copy-in and the last copy-out on the critical path). Instead, the
-// pages under the call's rows are registered with HIP for the duration of the
-// call (hipHostRegister, mapped: ~0.6 us per row) and the zero-copy kernel
-// reads the inputs and writes the outputs across the host link in place; the
-// pages are unregistered once the kernel has completed. tools/register_zc_probe.cpp,
-// one process, interleaved (profiles/r05/NOTES.md): encode 0.262 ms vs 0.325
-// staged, decode 0.239 vs 0.268. Taken when zero copy is on, every row is
-// 16-byte aligned (the vector kernels; a JVM places a 1 MiB byte[]'s data 16
-// bytes past a G1 region start), len >= HRS_HOST_DIRECT_MIN (64 KiB: below it
-// the copies cost less than the registrations), a checksummed call's kernel
-// is one-pass (a two-pass CRC would read the cells across the link twice),
-// and every range registers (pages another call or the caller already
-// registered fail it: the call then takes the staged path, same results).
-// HRS_HOST_DIRECT=0 turns it off (A/B runs and the staged-path tests; read per call).
+// caller's rows are made visible to the GPU for the call and the zero-copy
+// kernel reads the inputs and writes the outputs in place:
+//   - only pages that lie wholly inside a row are registered (hipHostRegister,
+//     mapped; ~0.6 us per row), so no page holding anyone else's bytes is
+//     ever registered (a pageable HIP copy by other code that touched such a
+//     page during the call would otherwise fail);
+//   - the columns every row has inside its whole pages, [c0, c1) with c1 - c0
+//     a multiple of 2 KiB, run over the caller's rows; the head [0, c0) and
+//     the tail [c1, len) (each under 4 KiB + 2 KiB) are copied through the
+//     pinned staging and run as small launches on a second stream, beside
+//     the middle's;
+//   - block CRCs: each of the three column segments yields its own raw CRC,
+//     chained on the host in column order (CRC32.update);
+//   - the pages are unregistered once the stream has drained.
+// A JVM's 1 MiB byte[] is a G1 humongous object whose data starts 16 bytes
+// past its region start: head 4,080 B, tail 16 B, middle 510 windows.
+// tools/register_zc_probe.cpp and tools/host_call_rate.cpp (profiles/r05/
+// NOTES.md): encode 0.25 ms vs 0.31-0.34 staged, decode 0.22 vs 0.27-0.30.
+// Taken when zero copy is on, every row is 16-byte aligned, len >=
+// HRS_HOST_DIRECT_MIN (64 KiB: below it the copies cost less than the
+// registrations), the middle spans at least 32 KiB, a checksummed call's
+// middle kernel is one-pass (a two-pass CRC would read the cells across the
+// link twice), no other call of this process holds any of its pages
+// (PageClaims) and every range registers (pages the caller registered fail
+// it). Otherwise the call takes the staged path, with the same results. HRS_HOST_DIRECT=0 turns it off (A/B runs; read per call).
 bool host_direct_on() {
   const char* e = getenv("HRS_HOST_DIRECT");
   return !(e && e[0] == '0');
@@ -126,27 +139,69 @@ size_t host_direct_min() {
   return v;
 }
 
+// The page ranges this library holds registered, process-wide. HIP accepts
+// a second hipHostRegister of pageable pages that are already registered, and
+// then the first unregister leaves the second call's kernel without its
+// mapping (and the second unregister aborts in the runtime's memory-object
+// map). Calls on different handles may share input rows (one stripe read by
+// several threads), so a call claims its ranges here first. A range that
+// overlaps one another call holds makes the call take the staged path.
+class PageClaims {
+ public:
+  static PageClaims& instance() {
+    static PageClaims p;
+    return p;
+  }
+  bool claim(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& r : rg) {
+      auto it = held_.lower_bound(r.first);  // first held range starting at or after r.first
+      if (it != held_.end() && it->first < r.second) return false;
+      if (it != held_.begin() && std::prev(it)->second > r.first) return false;
+    }
+    for (const auto& r : rg) held_.emplace(r.first, r.second);
+    return true;
+  }
+  void release(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& r : rg) held_.erase(r.first);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<uintptr_t, uintptr_t> held_;  // start -> end, disjoint
+};
+
 // Runs the call over the caller's rows; false (nothing done, nothing left
 // registered) when the call must take the staged path. *st: its status.
 bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
                        uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc, int nlive,
                        hrs_status* st) {
   if (!host_direct_on() || !zero_copy_on() || len < host_direct_min()) return false;
-  if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, len, 1)) return false;
-  if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, len)) return false;
   constexpr uintptr_t kPage = 4096;
-  std::vector<std::pair<uintptr_t, uintptr_t>> rg;
-  auto add = [&](const void* p) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    rg.push_back({a & ~(kPage - 1), (a + len + kPage - 1) & ~(kPage - 1)});
-    return aligned16(p);
-  };
+  constexpr size_t kMinMid = 32u << 10;
+  // the rows the call touches: live inputs, then outputs
+  std::vector<uintptr_t> rows;
   for (int i = 0; i < nin; ++i)
-    if (din[i] && !add(din[i])) return false;
-  for (int o = 0; o < nout; ++o)
-    if (!add(out_rows[o])) return false;
+    if (din[i]) rows.push_back(reinterpret_cast<uintptr_t>(din[i]));
+  for (int o = 0; o < nout; ++o) rows.push_back(reinterpret_cast<uintptr_t>(out_rows[o]));
+  size_t c0 = 0, tmax = 0;
+  for (uintptr_t a : rows) {
+    if (a & 15) return false;  // the vector kernels need 16-byte rows
+    c0 = std::max<size_t>(c0, (kPage - (a & (kPage - 1))) & (kPage - 1));
+    tmax = std::max<size_t>(tmax, (a + len) & (kPage - 1));
+  }
+  if (len < c0 + tmax + kMinMid) return false;
+  const size_t mid = (len - c0 - tmax) / hrs::kWindowBytes * hrs::kWindowBytes;
+  const size_t c1 = c0 + mid, tlen = len - c1;
+  if (mid < kMinMid) return false;
+  if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, mid, 1)) return false;
+  if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, mid)) return false;
+  // registration ranges: the whole pages of each row under [c0, c1)
+  std::vector<std::pair<uintptr_t, uintptr_t>> rg;
+  for (uintptr_t a : rows) rg.push_back({(a + c0) & ~(kPage - 1), (a + c1 + kPage - 1) & ~(kPage - 1)});
   std::sort(rg.begin(), rg.end());
-  size_t w = 0;  // merge ranges that share pages (rows of one heap region)
+  size_t w = 0;  // one range per row; a row passed twice (aliased rows) merges
   for (size_t r = 1; r < rg.size(); ++r) {
     if (rg[r].first < rg[w].second)
       rg[w].second = std::max(rg[w].second, rg[r].second);
@@ -154,16 +209,19 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
       rg[++w] = rg[r];
   }
   rg.resize(rg.empty() ? 0 : w + 1);
-  // the stream and, for checksums, the CRC words and scratch, before any page is registered
-  hrs_status s0 = host_slot(c, 0, 0);
-  if (s0 == HRS_OK && ncrc > 0 && !c->direct_crc) {
-    hipError_t e = hipHostMalloc(&c->direct_crc, 1024 * sizeof(uint32_t), hipHostMallocDefault);
-    if (e != hipSuccess) s0 = fail(c, HRS_ENOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
-    uint8_t* d = nullptr;
-    if (s0 == HRS_OK && host_device_ptr(c->direct_crc, &d)) c->direct_crc_dev = reinterpret_cast<uint32_t*>(d);
-  }
-  if (s0 == HRS_OK && ncrc > 0 && !c->direct_crc_dev) return false;
-  const size_t raw_need = ncrc > 0 ? crc_raw_bytes_for(len, 1, ncrc) : 0;
+  // staging for the head and tail columns (pinned, device-mapped), their CRC
+  // words, and the raw window-CRC scratch: all before any page is registered
+  const int nrows = nlive + nout;
+  const size_t ph = pitch_for(std::max<size_t>(c0, 1)), pt = pitch_for(std::max<size_t>(tlen, 1));
+  const size_t tail_off = ph * nrows, crc_off = tail_off + pt * nrows;
+  const size_t need = crc_off + 3 * static_cast<size_t>(std::max(ncrc, 1)) * sizeof(uint32_t);
+  hrs_status s0 = host_slot(c, 0, need);
+  if (s0 == HRS_OK && !c->host[0].pin_dev) return false;  // staging not device-mapped at its own address
+  // raw window-CRC scratch: the middle's, then the head / tail's (they run
+  // at the same time on two streams)
+  const size_t raw_mid = ncrc > 0 ? (crc_raw_bytes_for(mid, 1, ncrc) + 255) & ~static_cast<size_t>(255) : 0;
+  const size_t raw_need = ncrc > 0 ? raw_mid + crc_raw_bytes_for(std::max<size_t>({c0, tlen, 1}), 1, ncrc) : 0;
+  if (s0 == HRS_OK && (c0 || tlen)) s0 = host_slot(c, 1, 0);  // the head / tail stream
   if (s0 == HRS_OK && raw_need > c->direct_raw_bytes) {
     if (c->direct_raw) (void)hipFree(c->direct_raw);  // no call of this handle is in flight
     c->direct_raw = nullptr;
@@ -176,9 +234,11 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     *st = s0;
     return true;
   }
+  if (!PageClaims::instance().claim(rg)) return false;  // another call holds some of these pages
   std::vector<uintptr_t> held;
   auto release = [&] {
     for (uintptr_t a : held) (void)hipHostUnregister(reinterpret_cast<void*>(a));
+    PageClaims::instance().release(rg);
   };
   for (const auto& r : rg) {
     if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first, hipHostRegisterMapped) != hipSuccess) {
@@ -195,25 +255,72 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
       return false;
     }
   }
-  const hipStream_t s = c->host[0].stream;
+  hrs_codec::HostSlot& h = c->host[0];
+  const hipStream_t s = h.stream, s_ht = c->host[1].stream;
   c->last_host_path = "direct";
-  hrs_status rs;
+  // segment row pointers: head / tail rows in the staging (live inputs first,
+  // then outputs, as `rows`), middle rows in the caller's memory
+  std::vector<const uint8_t*> in_h(nin, nullptr), in_m(nin, nullptr), in_t(nin, nullptr);
+  std::vector<uint8_t*> out_h(nout), out_m(nout), out_t(nout);
+  {
+    int j = 0;
+    for (int i = 0; i < nin; ++i) {
+      if (!din[i]) continue;
+      in_h[i] = h.pin_dev + ph * j;
+      in_m[i] = din[i] + c0;
+      in_t[i] = h.pin_dev + tail_off + pt * j;
+      if (c0) std::memcpy(h.pin + ph * j, din[i], c0);
+      if (tlen) std::memcpy(h.pin + tail_off + pt * j, din[i] + c1, tlen);
+      ++j;
+    }
+    for (int o = 0; o < nout; ++o, ++j) {
+      out_h[o] = h.pin_dev + ph * j;
+      out_m[o] = out_rows[o] + c0;
+      out_t[o] = h.pin_dev + tail_off + pt * j;
+    }
+  }
+  uint32_t* crc_dev = reinterpret_cast<uint32_t*>(h.pin_dev + crc_off);
+  auto segment = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, size_t sl, int seg,
+                     hipStream_t ss, uint32_t* raw) -> hrs_status {
+    uint32_t* cw = crc_dev + seg * ncrc;
+    if (crc.mode == kCrcEncode) return encode_crc_impl(c, in.data(), 0, out.data(), 0, sl, 1, nullptr, cw, ss, raw);
+    if (crc.mode == kCrcOutputs)
+      return apply_crc_impl(c, m, nout, nin, in.data(), 0, out.data(), 0, sl, 1, nullptr, cw, ss, raw);
+    return run_apply(c, m, nout, nin, in.data(), 0, out.data(), 0, sl, 1, ss, static_kp);
+  };
+  // the middle first, on slot 0's stream; the small head and tail launches
+  // follow on slot 1's, so they run beside the middle instead of after it
+  uint32_t* raw_ht = c->direct_raw ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(c->direct_raw) + raw_mid)
+                                   : nullptr;
+  hrs_status rs = HRS_OK;
   {
     hrs::GridCap cap(zero_copy_blocks());
-    if (crc.mode == kCrcEncode)
-      rs = encode_crc_impl(c, din, 0, out_rows, 0, len, 1, nullptr, c->direct_crc_dev, s, c->direct_raw);
-    else if (crc.mode == kCrcOutputs)
-      rs = apply_crc_impl(c, m, nout, nin, din, 0, out_rows, 0, len, 1, nullptr, c->direct_crc_dev, s, c->direct_raw);
-    else
-      rs = run_apply(c, m, nout, nin, din, 0, out_rows, 0, len, 1, s, static_kp);
+    rs = segment(in_m, out_m, mid, 1, s, c->direct_raw);
+    if (rs == HRS_OK && c0) rs = segment(in_h, out_h, c0, 0, s_ht, raw_ht);
+    if (rs == HRS_OK && tlen) rs = segment(in_t, out_t, tlen, 2, s_ht, raw_ht);
   }
-  // whatever the launch did, nothing may touch the pages once they are unregistered
-  const hipError_t e = hipStreamSynchronize(s);
+  // whatever the launches did, nothing may touch the pages once they are unregistered
+  hipError_t e = hipStreamSynchronize(s);
   if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
+  if (c0 || tlen) {
+    e = hipStreamSynchronize(s_ht);
+    if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
+  }
   release();
-  if (rs == HRS_OK && ncrc > 0) {  // CRC32.update chaining: crc = Z_len(crc) ^ crc(cell)
-    const hrs::crc::Mat& z = crc_zmat(c, len);
-    for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ c->direct_crc[r];
+  if (rs == HRS_OK) {
+    for (int o = 0; o < nout; ++o) {
+      const int j = nlive + o;
+      if (c0) std::memcpy(out_rows[o], h.pin + ph * j, c0);
+      if (tlen) std::memcpy(out_rows[o] + c1, h.pin + tail_off + pt * j, tlen);
+    }
+    // CRC32.update chaining over the three column segments in order
+    const uint32_t* part = reinterpret_cast<const uint32_t*>(h.pin + crc_off);
+    const size_t seg_len[3] = {c0, mid, tlen};
+    for (int seg = 0; seg < 3 && ncrc > 0; ++seg) {
+      if (!seg_len[seg]) continue;
+      const hrs::crc::Mat& z = crc_zmat(c, seg_len[seg]);
+      for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[seg * ncrc + r];
+    }
   }
   *st = rs;
   return true;

@@ -4,9 +4,11 @@ the call and the zero-copy kernel reads the inputs and writes the outputs in
 place (hrs_hostpath.cpp host_apply_direct), instead of the staged copies.
 Checked against the oracle (ReedSolomonCode.encodeBulk / decodeBulk 5-arg,
 ReedSolomonCode.java:103-125, :191-211) and zlib, for the row layouts a JNI
-caller produces, and for every case that must fall back to the staged path
-(misaligned rows, pages already pinned, short rows, concurrent calls whose
-rows share pages). hrs_last_host_path says which path a call took."""
+caller produces (rows sharing pages with their neighbours included: only
+pages wholly inside a row are registered, the head and tail columns go
+through the staging), and for every case that must fall back to the staged
+path (misaligned rows, pages already pinned, short rows).
+hrs_last_host_path says which path a call took."""
 import threading
 import zlib
 
@@ -55,7 +57,8 @@ def test_direct_separate_rows(cuda):
 
 def test_direct_rows_sharing_pages(cuda):
     """Rows laid out like small heap objects: 16-byte headers between them,
-    so neighbouring rows share pages (one merged registration)."""
+    so neighbouring rows share pages. Only the pages wholly inside a row are
+    registered; the columns in the shared pages go through the staging."""
     code = HipReedSolomonCode(K, P, zero_inputs_after_encode=False)
     n = K + P
     Ls = (256 << 10) + 48  # a multiple of 16: every row stays 16-byte aligned
@@ -132,8 +135,9 @@ def test_direct_checksummed_calls(cuda):
 
 def test_concurrent_calls_rows_sharing_pages(cuda):
     """Four threads, one codec each (one Encoder per mapper thread), whose
-    rows are neighbours in one buffer: a call whose pages another call holds
-    registered takes the staged path; every result is bit-exact either way."""
+    rows are neighbours in one buffer (pages shared between the threads' rows):
+    no call registers a page another row reaches into, so the calls run
+    direct side by side; every result is bit-exact."""
     n = K + P
     Ls = (128 << 10) + 16
     T, R = 4, 6
@@ -165,3 +169,41 @@ def test_concurrent_calls_rows_sharing_pages(cuda):
     if errs:
         raise errs[0]
     assert set(paths) <= {"direct", "staged"} and "direct" in paths
+
+
+def test_concurrent_calls_sharing_input_rows(cuda):
+    """Four threads encode the SAME input rows at once (a stripe read by
+    several codecs): HIP would accept the same pages registered twice and
+    then drop the mapping under the other call, so each call first claims its
+    pages process-wide (PageClaims); a call that finds them held takes the
+    staged path. Every result is bit-exact and the process stays healthy."""
+    T, R = 4, 8
+    rng = np.random.default_rng(8)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(K)]
+    ref = C.encode_bulk(K, P, [np.array(d) for d in data])
+    errs, paths = [], []
+
+    def body(t):
+        try:
+            code = HipReedSolomonCode(K, P, zero_inputs_after_encode=False)
+            par = [np.zeros(L, np.uint8) for _ in range(P)]
+            for _ in range(R):
+                code.encodeBulk(data, par)
+                paths.append(code.lastHostPath())
+                if not all(np.array_equal(par[o], ref[o]) for o in range(P)):
+                    raise AssertionError(f"thread {t}: parity differs ({code.lastHostPath()} path)")
+        except Exception as e:  # noqa: BLE001 - reported after the join
+            errs.append(e)
+
+    ths = [threading.Thread(target=body, args=(t,)) for t in range(T)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    if errs:
+        raise errs[0]
+    assert set(paths) <= {"direct", "staged"} and len(paths) == T * R
+    code = HipReedSolomonCode(K, P, zero_inputs_after_encode=False)
+    par = [np.zeros(L, np.uint8) for _ in range(P)]
+    code.encodeBulk(data, par)  # every claim was released
+    assert code.lastHostPath() == "direct"
