@@ -20,7 +20,7 @@ API_OBJ  := $(patsubst %,build/%.o,$(API_SRC))
 
 JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
-            tests/cpp/copy_pool_test
+            tests/cpp/copy_pool_test tests/cpp/page_claims_test
 
 TOOLS    := tools/host_call_rate tools/register_zc_probe
 
@@ -112,6 +112,10 @@ tests/cpp/crc_tables: tests/cpp/crc_tables.cpp lambdafs_amd/csrc/crc32.hpp lambd
 tests/cpp/copy_pool_test: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
 	g++ -O2 -std=c++17 -Wall -pthread -o $@ $<
 
+# The direct calls' process-wide page claims under concurrent holders (CPU only).
+tests/cpp/page_claims_test: tests/cpp/page_claims_test.cpp lambdafs_amd/csrc/hrs_host.hpp
+	g++ -O2 -std=c++17 -Wall -pthread -o $@ $<
+
 tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
 	g++ -O2 -std=c++17 -Wall -o $@ $< -lz
 
@@ -166,11 +170,12 @@ asan: $(ASAN_BIN)
 
 # ---- make tsan: the host copy pool (hrs_host.hpp: concurrent callers,
 # spinning workers that drain the batches they join) under ThreadSanitizer.
-TSAN_LOG := profiles/r04/tsan
-tsan: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
+TSAN_LOG := profiles/r05/tsan
+tsan: tests/cpp/copy_pool_test.cpp tests/cpp/page_claims_test.cpp lambdafs_amd/csrc/hrs_host.hpp
 	@mkdir -p build/tsan $(TSAN_LOG)
 	g++ -O1 -g -std=c++17 -fsanitize=thread -pthread -o build/tsan/copy_pool_test tests/cpp/copy_pool_test.cpp
-	sh -c 'for t in 0 1 4 8; do HRS_HOST_THREADS=$$t build/tsan/copy_pool_test 4 20; done' > $(TSAN_LOG)/tsan_run.log 2>&1 || { cat $(TSAN_LOG)/tsan_run.log; exit 1; }
+	g++ -O1 -g -std=c++17 -fsanitize=thread -pthread -o build/tsan/page_claims_test tests/cpp/page_claims_test.cpp
+	sh -c 'for t in 0 1 4 8; do HRS_HOST_THREADS=$$t build/tsan/copy_pool_test 4 20; done; build/tsan/page_claims_test 8 5000' > $(TSAN_LOG)/tsan_run.log 2>&1 || { cat $(TSAN_LOG)/tsan_run.log; exit 1; }
 	@cat $(TSAN_LOG)/tsan_run.log
 
 clean:

@@ -12,6 +12,9 @@
 // none is left (a piece per lock round trip cost a 5 MiB copy-in 40-80 us on
 // the MI355X hosts whatever the worker count: tools/pool_probe.cpp). A call
 // returns once all its pieces are copied and no worker still holds its batch.
+//
+// Also the process-wide claims on host page ranges the synchronous calls
+// register with HIP for their duration (PageClaims, hrs_hostpath.cpp).
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -22,6 +25,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -176,6 +180,39 @@ class CopyPool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   bool stop_ = false;
+};
+
+// The page ranges this library holds registered, process-wide. HIP accepts
+// a second hipHostRegister of pageable pages that are already registered, and
+// then the first unregister leaves the second call's kernel without its
+// mapping (and the second unregister aborts in the runtime's memory-object
+// map). Calls on different handles may share input rows (one stripe read by
+// several threads), so a call claims its ranges here first. A range that
+// overlaps one another call holds makes the call take the staged path.
+class PageClaims {
+ public:
+  static PageClaims& instance() {
+    static PageClaims p;
+    return p;
+  }
+  bool claim(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& r : rg) {
+      auto it = held_.lower_bound(r.first);  // first held range starting at or after r.first
+      if (it != held_.end() && it->first < r.second) return false;
+      if (it != held_.begin() && std::prev(it)->second > r.first) return false;
+    }
+    for (const auto& r : rg) held_.emplace(r.first, r.second);
+    return true;
+  }
+  void release(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& r : rg) held_.erase(r.first);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<uintptr_t, uintptr_t> held_;  // start -> end, disjoint
 };
 
 }  // namespace hrs

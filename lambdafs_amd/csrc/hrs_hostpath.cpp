@@ -8,7 +8,6 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -139,39 +138,6 @@ size_t host_direct_min() {
   return v;
 }
 
-// The page ranges this library holds registered, process-wide. HIP accepts
-// a second hipHostRegister of pageable pages that are already registered, and
-// then the first unregister leaves the second call's kernel without its
-// mapping (and the second unregister aborts in the runtime's memory-object
-// map). Calls on different handles may share input rows (one stripe read by
-// several threads), so a call claims its ranges here first. A range that
-// overlaps one another call holds makes the call take the staged path.
-class PageClaims {
- public:
-  static PageClaims& instance() {
-    static PageClaims p;
-    return p;
-  }
-  bool claim(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (const auto& r : rg) {
-      auto it = held_.lower_bound(r.first);  // first held range starting at or after r.first
-      if (it != held_.end() && it->first < r.second) return false;
-      if (it != held_.begin() && std::prev(it)->second > r.first) return false;
-    }
-    for (const auto& r : rg) held_.emplace(r.first, r.second);
-    return true;
-  }
-  void release(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (const auto& r : rg) held_.erase(r.first);
-  }
-
- private:
-  std::mutex mu_;
-  std::map<uintptr_t, uintptr_t> held_;  // start -> end, disjoint
-};
-
 // Runs the call over the caller's rows; false (nothing done, nothing left
 // registered) when the call must take the staged path. *st: its status.
 bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
@@ -234,11 +200,11 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     *st = s0;
     return true;
   }
-  if (!PageClaims::instance().claim(rg)) return false;  // another call holds some of these pages
+  if (!hrs::PageClaims::instance().claim(rg)) return false;  // another call holds some of these pages
   std::vector<uintptr_t> held;
   auto release = [&] {
     for (uintptr_t a : held) (void)hipHostUnregister(reinterpret_cast<void*>(a));
-    PageClaims::instance().release(rg);
+    hrs::PageClaims::instance().release(rg);
   };
   for (const auto& r : rg) {
     if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first, hipHostRegisterMapped) != hipSuccess) {

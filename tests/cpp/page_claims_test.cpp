@@ -1,0 +1,83 @@
+// hrs::PageClaims (hrs_host.hpp): the process-wide claims on host page ranges
+// the synchronous direct calls register with HIP (hrs_hostpath.cpp). Checks the
+// overlap rules single-threaded, then N threads claiming random ranges of a
+// small page space at once: a claimed page is never claimed by a second
+// holder, and every claim is released. CPU only (also under `make tsan`).
+// Usage: page_claims_test [threads] [iterations]   (one JSON line)
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "../../lambdafs_amd/csrc/hrs_host.hpp"
+
+using Ranges = std::vector<std::pair<uintptr_t, uintptr_t>>;
+
+int main(int argc, char** argv) {
+  const int nthreads = argc > 1 ? atoi(argv[1]) : 4;
+  const int iters = argc > 2 ? atoi(argv[2]) : 20000;
+  const uintptr_t P = 4096, base = uintptr_t(1) << 40;
+  hrs::PageClaims& pc = hrs::PageClaims::instance();
+  int bad = 0;
+  auto R = [&](int a, int b) { return std::make_pair(base + a * P, base + b * P); };
+  // rules: overlap fails, adjacency is fine, release frees, all-or-nothing
+  bad += !pc.claim({R(10, 20)});
+  bad += pc.claim({R(15, 16)});           // inside
+  bad += pc.claim({R(5, 11)});            // overlaps the start
+  bad += pc.claim({R(19, 30)});           // overlaps the end
+  bad += pc.claim({R(0, 100)});           // covers it
+  bad += !pc.claim({R(20, 21), R(9, 10)});  // adjacent on both sides
+  bad += pc.claim({R(30, 31), R(12, 13)});  // one of two overlaps: nothing claimed
+  bad += !pc.claim({R(30, 31)});            // ... so this one is still free
+  pc.release({R(10, 20)});
+  bad += !pc.claim({R(15, 16)});
+  pc.release({R(15, 16)});
+  pc.release({R(20, 21), R(9, 10)});
+  pc.release({R(30, 31)});
+  bad += !pc.claim({R(0, 100)});
+  pc.release({R(0, 100)});
+  // concurrent holders over a 64-page space
+  const int npages = 64;
+  std::vector<std::atomic<int>> owner(npages);
+  for (auto& o : owner) o = -1;
+  std::atomic<int> violations{0};
+  std::atomic<long> granted{0}, refused{0};
+  auto body = [&](int t) {
+    std::mt19937 rng(1234 + t);
+    for (int it = 0; it < iters; ++it) {
+      Ranges rg;
+      const int nr = 1 + rng() % 3;
+      for (int r = 0; r < nr; ++r) {
+        const int a = rng() % (npages - 4), len = 1 + rng() % 4;
+        bool dup = false;  // ranges of one call are disjoint (the caller merges them)
+        for (auto& x : rg) dup |= !(R(a, a + len).second <= x.first || x.second <= R(a, a + len).first);
+        if (!dup) rg.push_back(R(a, a + len));
+      }
+      if (!pc.claim(rg)) {
+        refused++;
+        continue;
+      }
+      granted++;
+      for (auto& x : rg)
+        for (uintptr_t pg = (x.first - base) / P; pg < (x.second - base) / P; ++pg) {
+          int expect = -1;
+          if (!owner[pg].compare_exchange_strong(expect, t)) violations++;
+        }
+      for (auto& x : rg)
+        for (uintptr_t pg = (x.first - base) / P; pg < (x.second - base) / P; ++pg) owner[pg] = -1;
+      pc.release(rg);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) th.emplace_back(body, t);
+  for (auto& x : th) x.join();
+  bad += !pc.claim({R(0, npages)});  // every claim was released
+  pc.release({R(0, npages)});
+  const bool ok = bad == 0 && violations == 0;
+  printf("{\"threads\": %d, \"iterations\": %d, \"rule_failures\": %d, \"violations\": %d, \"granted\": %ld, "
+         "\"refused\": %ld, \"ok\": %s}\n",
+         nthreads, iters, bad, violations.load(), granted.load(), refused.load(), ok ? "true" : "false");
+  return ok ? 0 : 1;
+}
