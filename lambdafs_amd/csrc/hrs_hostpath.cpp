@@ -108,15 +108,16 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
 //   - the columns every row has inside its whole pages, [c0, c1) with c1 - c0
 //     a multiple of 2 KiB, run over the caller's rows; the head [0, c0) and
 //     the tail [c1, len) (each under 4 KiB + 2 KiB) are copied through the
-//     pinned staging and run as small launches on a second stream, beside
-//     the middle's;
-//   - block CRCs: each of the three column segments yields its own raw CRC,
+//     pinned staging and run as ONE small two-stripe launch on a second
+//     stream, beside the middle's (separate head and tail launches, and the
+//     two-pass CRC their ragged widths needed, cost 0.03-0.10 ms per call);
+//   - block CRCs: each of the three column segments yields its own CRC,
 //     chained on the host in column order (CRC32.update);
 //   - the pages are unregistered once the stream has drained.
 // A JVM's 1 MiB byte[] is a G1 humongous object whose data starts 16 bytes
 // past its region start: head 4,080 B, tail 16 B, middle 510 windows.
-// tools/register_zc_probe.cpp and tools/host_call_rate.cpp (profiles/r05/
-// NOTES.md): encode 0.25 ms vs 0.31-0.34 staged, decode 0.22 vs 0.27-0.30.
+// tools/host_call_rate.cpp (profiles/r05/NOTES.md): encode 0.27 ms vs 0.36
+// staged, encode + CRC 0.29 vs 0.38, decode 0.25 vs 0.31.
 // Taken when zero copy is on, every row is 16-byte aligned, len >=
 // HRS_HOST_DIRECT_MIN (64 KiB: below it the copies cost less than the
 // registrations), the middle spans at least 32 KiB, a checksummed call's
@@ -176,18 +177,26 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
   }
   rg.resize(rg.empty() ? 0 : w + 1);
   // staging for the head and tail columns (pinned, device-mapped), their CRC
-  // words, and the raw window-CRC scratch: all before any page is registered
+  // words, and the raw window-CRC scratch: all before any page is registered.
+  // The head and the tail run as ONE launch of two "stripes" (stripe 0 the
+  // head, 1 the tail) of W-byte staging rows, each segment right-aligned
+  // behind a zero pad: columns are independent, a raw CRC ignores leading
+  // zeros, and W is a whole number of 2 KiB windows, so a checksummed call's
+  // head / tail take the fused kernel too (the pad's length term in the CRC is
+  // taken out on the host, pad_fix).
   const int nrows = nlive + nout;
-  const size_t ph = pitch_for(std::max<size_t>(c0, 1)), pt = pitch_for(std::max<size_t>(tlen, 1));
-  const size_t tail_off = ph * nrows, crc_off = tail_off + pt * nrows;
+  const size_t W = (c0 || tlen) ? (std::max(c0, tlen) + hrs::kWindowBytes - 1) / hrs::kWindowBytes * hrs::kWindowBytes
+                                : 0;
+  const size_t ht_stride = W * nrows;  // head stripe, then tail stripe
+  const size_t crc_off = 2 * ht_stride;
   const size_t need = crc_off + 3 * static_cast<size_t>(std::max(ncrc, 1)) * sizeof(uint32_t);
   hrs_status s0 = host_slot(c, 0, need);
   if (s0 == HRS_OK && !c->host[0].pin_dev) return false;  // staging not device-mapped at its own address
   // raw window-CRC scratch: the middle's, then the head / tail's (they run
   // at the same time on two streams)
   const size_t raw_mid = ncrc > 0 ? (crc_raw_bytes_for(mid, 1, ncrc) + 255) & ~static_cast<size_t>(255) : 0;
-  const size_t raw_need = ncrc > 0 ? raw_mid + crc_raw_bytes_for(std::max<size_t>({c0, tlen, 1}), 1, ncrc) : 0;
-  if (s0 == HRS_OK && (c0 || tlen)) s0 = host_slot(c, 1, 0);  // the head / tail stream
+  const size_t raw_need = ncrc > 0 ? raw_mid + crc_raw_bytes_for(std::max<size_t>(W, 1), 2, ncrc) : 0;
+  if (s0 == HRS_OK && W) s0 = host_slot(c, 1, 0);  // the head / tail stream
   if (s0 == HRS_OK && raw_need > c->direct_raw_bytes) {
     if (c->direct_raw) (void)hipFree(c->direct_raw);  // no call of this handle is in flight
     c->direct_raw = nullptr;
@@ -224,68 +233,82 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
   hrs_codec::HostSlot& h = c->host[0];
   const hipStream_t s = h.stream, s_ht = c->host[1].stream;
   c->last_host_path = "direct";
-  // segment row pointers: head / tail rows in the staging (live inputs first,
-  // then outputs, as `rows`), middle rows in the caller's memory
-  std::vector<const uint8_t*> in_h(nin, nullptr), in_m(nin, nullptr), in_t(nin, nullptr);
-  std::vector<uint8_t*> out_h(nout), out_m(nout), out_t(nout);
+  // row pointers: the middle's in the caller's memory; the head / tail's in
+  // the staging (live inputs first, then outputs, as `rows`), row j of
+  // stripe t at t * ht_stride + j * W, its segment in the last bytes
+  std::vector<const uint8_t*> in_ht(nin, nullptr), in_m(nin, nullptr);
+  std::vector<uint8_t*> out_ht(nout), out_m(nout);
   {
     int j = 0;
     for (int i = 0; i < nin; ++i) {
       if (!din[i]) continue;
-      in_h[i] = h.pin_dev + ph * j;
       in_m[i] = din[i] + c0;
-      in_t[i] = h.pin_dev + tail_off + pt * j;
-      if (c0) std::memcpy(h.pin + ph * j, din[i], c0);
-      if (tlen) std::memcpy(h.pin + tail_off + pt * j, din[i] + c1, tlen);
+      if (W) {
+        in_ht[i] = h.pin_dev + W * j;
+        uint8_t* hr = h.pin + W * j;
+        uint8_t* tr = hr + ht_stride;
+        if (ncrc > 0) {  // the CRC reads the pads: zeros
+          std::memset(hr, 0, W - c0);
+          std::memset(tr, 0, W - tlen);
+        }
+        std::memcpy(hr + (W - c0), din[i], c0);
+        std::memcpy(tr + (W - tlen), din[i] + c1, tlen);
+      }
       ++j;
     }
     for (int o = 0; o < nout; ++o, ++j) {
-      out_h[o] = h.pin_dev + ph * j;
       out_m[o] = out_rows[o] + c0;
-      out_t[o] = h.pin_dev + tail_off + pt * j;
+      out_ht[o] = h.pin_dev + W * j;
     }
   }
-  uint32_t* crc_dev = reinterpret_cast<uint32_t*>(h.pin_dev + crc_off);
-  auto segment = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, size_t sl, int seg,
-                     hipStream_t ss, uint32_t* raw) -> hrs_status {
-    uint32_t* cw = crc_dev + seg * ncrc;
-    if (crc.mode == kCrcEncode) return encode_crc_impl(c, in.data(), 0, out.data(), 0, sl, 1, nullptr, cw, ss, raw);
+  uint32_t* crc_dev = reinterpret_cast<uint32_t*>(h.pin_dev + crc_off);  // head, tail, middle: ncrc words each
+  auto segment = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, size_t stride,
+                     size_t sl, size_t nst, uint32_t* cw, hipStream_t ss, uint32_t* raw) -> hrs_status {
+    if (crc.mode == kCrcEncode)
+      return encode_crc_impl(c, in.data(), stride, out.data(), stride, sl, nst, nullptr, cw, ss, raw);
     if (crc.mode == kCrcOutputs)
-      return apply_crc_impl(c, m, nout, nin, in.data(), 0, out.data(), 0, sl, 1, nullptr, cw, ss, raw);
-    return run_apply(c, m, nout, nin, in.data(), 0, out.data(), 0, sl, 1, ss, static_kp);
+      return apply_crc_impl(c, m, nout, nin, in.data(), stride, out.data(), stride, sl, nst, nullptr, cw, ss, raw);
+    return run_apply(c, m, nout, nin, in.data(), stride, out.data(), stride, sl, nst, ss, static_kp);
   };
-  // the middle first, on slot 0's stream; the small head and tail launches
-  // follow on slot 1's, so they run beside the middle instead of after it
+  // the middle first, on slot 0's stream; the small head / tail launch
+  // follows on slot 1's, so it runs beside the middle instead of after it
   uint32_t* raw_ht = c->direct_raw ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(c->direct_raw) + raw_mid)
                                    : nullptr;
   hrs_status rs = HRS_OK;
   {
     hrs::GridCap cap(zero_copy_blocks());
-    rs = segment(in_m, out_m, mid, 1, s, c->direct_raw);
-    if (rs == HRS_OK && c0) rs = segment(in_h, out_h, c0, 0, s_ht, raw_ht);
-    if (rs == HRS_OK && tlen) rs = segment(in_t, out_t, tlen, 2, s_ht, raw_ht);
+    rs = segment(in_m, out_m, 0, mid, 1, crc_dev + 2 * ncrc, s, c->direct_raw);
+    if (rs == HRS_OK && W) rs = segment(in_ht, out_ht, ht_stride, W, 2, crc_dev, s_ht, raw_ht);
   }
   // whatever the launches did, nothing may touch the pages once they are unregistered
   hipError_t e = hipStreamSynchronize(s);
   if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
-  if (c0 || tlen) {
+  if (W) {
     e = hipStreamSynchronize(s_ht);
     if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
   }
   release();
   if (rs == HRS_OK) {
     for (int o = 0; o < nout; ++o) {
-      const int j = nlive + o;
-      if (c0) std::memcpy(out_rows[o], h.pin + ph * j, c0);
-      if (tlen) std::memcpy(out_rows[o] + c1, h.pin + tail_off + pt * j, tlen);
+      const uint8_t* hr = h.pin + W * (nlive + o);
+      std::memcpy(out_rows[o], hr + (W - c0), c0);
+      std::memcpy(out_rows[o] + c1, hr + ht_stride + (W - tlen), tlen);
     }
-    // CRC32.update chaining over the three column segments in order
+    // CRC32.update chaining over the three column segments in order. A
+    // padded segment's fold returned crc32(0, pad || D) = crc32(0, D) ^
+    // Z_W(~0) ^ Z_|D|(~0) (crc32.hpp: the raw part ignores leading zeros)
     const uint32_t* part = reinterpret_cast<const uint32_t*>(h.pin + crc_off);
+    auto pad_fix = [&](size_t d) {
+      return hrs::crc::apply(crc_zmat(c, W), ~0u) ^ hrs::crc::apply(crc_zmat(c, d), ~0u);
+    };
     const size_t seg_len[3] = {c0, mid, tlen};
+    const int seg_word[3] = {0, 2, 1};
     for (int seg = 0; seg < 3 && ncrc > 0; ++seg) {
       if (!seg_len[seg]) continue;
       const hrs::crc::Mat& z = crc_zmat(c, seg_len[seg]);
-      for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[seg * ncrc + r];
+      const uint32_t fix = seg == 1 ? 0u : pad_fix(seg_len[seg]);
+      for (int r = 0; r < ncrc; ++r)
+        crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[seg_word[seg] * ncrc + r] ^ fix;
     }
   }
   *st = rs;

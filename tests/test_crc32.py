@@ -29,6 +29,22 @@ def _u32(x):
     return int(x) & 0xFFFFFFFF
 
 
+@pytest.mark.parametrize("d,W", [(4080, 4096), (16, 4096), (1, 2048), (2048, 2048), (0, 2048), (5000, 6144)])
+def test_leading_pad_correction(d, W):
+    """The identity the direct host path (hrs_hostpath.cpp host_apply_direct,
+    pad_fix) uses for its head / tail segments, which it runs right-aligned
+    behind a zero pad: crc32(0, D) = crc32(0, 0^m || D) ^ Z_W(~0) ^ Z_d(~0),
+    with Z_n(~0) = ~crc32(0, 0^n) (a raw CRC ignores leading zeros; only the
+    length term differs)."""
+    D = np.random.default_rng(d).integers(0, 256, d, dtype=np.uint8).tobytes()
+    padded = bytes(W - d) + D
+
+    def z(n):
+        return ~zlib.crc32(bytes(n)) & 0xFFFFFFFF
+
+    assert zlib.crc32(D) == zlib.crc32(padded) ^ z(W) ^ z(d)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("L", [0, 1, 100, 4095, 4096, 4097, 65536 + 13, 1 << 20, (1 << 20) + 4096 * 70 + 33])
 def test_crc32_rows_match_zlib(cuda, L):

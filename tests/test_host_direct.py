@@ -133,6 +133,50 @@ def test_direct_checksummed_calls(cuda):
     assert dcrc == [zlib.crc32(data[0].tobytes(), 7) & 0xFFFFFFFF]
 
 
+def _page_rows(n, length, offset, rng):
+    """n rows, each `offset` bytes past a page boundary of its own buffer."""
+    rows = []
+    for _ in range(n):
+        raw = rng.integers(0, 256, length + offset + 8192, dtype=np.uint8)
+        base = (-raw.ctypes.data) % 4096
+        rows.append(raw[base + offset: base + offset + length])
+    return rows
+
+
+@pytest.mark.parametrize("offset", [0, 16, 2048, 4000])
+@pytest.mark.parametrize("length", [1 << 20, (1 << 20) + 784, (300 << 10) + 48])
+def test_direct_head_tail_shapes(cuda, offset, length):
+    """Head / tail columns of every width (none, 16 B, 2 KiB, 4,080 B; tails of
+    0 to ~6 KiB): they run as one two-stripe launch, right-aligned behind a
+    zero pad, and a checksummed call's segment CRCs are chained with the pad's
+    length term removed. Parity, repaired rows and CRCs vs the oracle / zlib."""
+    rng = np.random.default_rng(offset * 7 + length)
+    code = HipReedSolomonCode(K, P, zero_inputs_after_encode=False)
+    data = _page_rows(K, length, offset, rng)
+    par = _page_rows(P, length, offset, rng)
+    ref = C.encode_bulk(K, P, [np.array(d) for d in data])
+    code.encodeBulk(data, par)
+    assert code.lastHostPath() == "direct"
+    assert all(np.array_equal(par[o], ref[o]) for o in range(P))
+    for x in par:
+        x[:] = 0x3C
+    run = [int(x) for x in rng.integers(0, 1 << 32, K + P, dtype=np.uint64)]
+    crcs = code.encodeBulkCrc(data, par, run)
+    assert code.lastHostPath() == "direct"
+    assert all(np.array_equal(par[o], ref[o]) for o in range(P))
+    cells = data + list(ref)
+    assert crcs == [zlib.crc32(cells[i].tobytes(), run[i]) & 0xFFFFFFFF for i in range(K + P)]
+    stripe = list(ref) + data
+    erased = [P + 1, 2]
+    tr = sorted(C.locations_to_read(K, P, erased))
+    ntr = [x for x in range(K + P) if x not in tr]
+    outs = _page_rows(len(erased), length, offset, rng)
+    dcrc = code.decodeBulkCrc([stripe[i] if i in tr else None for i in range(K + P)], outs, erased, tr, ntr, [5, 6])
+    assert code.lastHostPath() == "direct"
+    assert all(np.array_equal(outs[j], stripe[e]) for j, e in enumerate(erased))
+    assert dcrc == [zlib.crc32(stripe[e].tobytes(), 5 + j) & 0xFFFFFFFF for j, e in enumerate(erased)]
+
+
 def test_concurrent_calls_rows_sharing_pages(cuda):
     """Four threads, one codec each (one Encoder per mapper thread), whose
     rows are neighbours in one buffer (pages shared between the threads' rows):
