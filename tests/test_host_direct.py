@@ -251,3 +251,117 @@ def test_concurrent_calls_sharing_input_rows(cuda):
     par = [np.zeros(L, np.uint8) for _ in range(P)]
     code.encodeBulk(data, par)  # every claim was released
     assert code.lastHostPath() == "direct"
+
+
+def _fz_code(fam, k, p, s):
+    from lambdafs_amd import HipNativeReedSolomonCode, HipSimpleRegeneratingCode, HipXORCode
+    code = {"rs": lambda: HipReedSolomonCode(k, p), "nrs": lambda: HipNativeReedSolomonCode(k, p),
+            "xor": lambda: HipXORCode(k, 1), "src": lambda: HipSimpleRegeneratingCode(k, p, s)}[fam]()
+    code.zero_inputs_after_encode = False
+    return code
+
+
+def _fz_encode_ref(fam, k, p, s, data):
+    if fam == "rs":
+        return C.encode_bulk(k, p, data)
+    if fam == "nrs":
+        return C.nrs_encode_bulk(k, p, data)
+    if fam == "xor":
+        return [C.xor_encode_bulk(k, data)]
+    return C.src_encode_bulk(k, p, s, data)
+
+
+def _fz_pattern(fam, k, p, s, rnd):
+    """(erased, not_to_read, to_read) as Decoder.java:303-338 builds them."""
+    n = k + p
+    while True:
+        if fam == "xor":
+            e = rnd.randrange(n)
+            return [e], [e], [x for x in range(n) if x != e]
+        if fam == "nrs":
+            m = rnd.randint(1, p)
+            ntr = sorted(rnd.sample(range(n), m))
+            return ntr[:rnd.randint(1, m)], ntr, [x for x in range(n) if x not in ntr]
+        erased = sorted(rnd.sample(range(n), rnd.randint(1, p)))
+        tr = C.locations_to_read(k, p, erased) if fam == "rs" else C.src_locations_to_read(k, p, s, erased)
+        if tr is not None:
+            tr = sorted(tr)
+            return erased, [x for x in range(n) if x not in tr or x in erased], tr
+
+
+def _fz_decode_ref(fam, k, p, s, reads, erased, ntr, tr):
+    if fam == "rs":
+        return C.decode_bulk5(k, p, reads, erased, tr, ntr)
+    if fam == "nrs":
+        return C.nrs_decode_bulk(k, p, reads, erased, ntr)
+    if fam == "xor":
+        return [C.xor_decode_bulk(k, reads, erased[0])]
+    return C.src_decode_bulk(k, p, s, reads, erased, tr, ntr)
+
+
+def test_direct_fuzz(cuda):
+    """Seeded differential fuzz of the synchronous host calls over the
+    caller's rows: code family (rs static / runtime shapes, nrs, xor, src) x
+    row length (64 KiB .. 1.3 MiB, ragged) x row placement (16-byte offsets
+    in a shared heap-like buffer, rows sharing pages) x call (encodeBulk,
+    decodeBulk 5-arg, encodeBulkCrc / decodeBulkCrc for rs, nrs and xor).
+    Non-codeword reads, bit-exact vs the oracle and zlib; at least half the
+    calls must take the direct path (the rest are the staged fallbacks)."""
+    import random
+    rnd = random.Random(0xD1EC7)
+    fams = ["rs", "rs", "nrs", "xor", "src"]
+    paths = []
+    for case in range(40):
+        fam = fams[case % len(fams)]
+        s = 0
+        if fam == "rs":
+            k, p = rnd.choice([(10, 4), (6, 3), (12, 4), (3, 2)]) if case % 2 else (rnd.randint(2, 14), rnd.randint(1, 5))
+        elif fam == "nrs":
+            k, p = rnd.choice([(10, 4), (6, 3), (rnd.randint(2, 12), rnd.randint(1, 4))])
+        elif fam == "xor":
+            k, p = rnd.randint(2, 12), 1
+        else:
+            k, p, s = rnd.choice([(10, 6, 2), (6, 3, 2), (10, 4, 3), (10, 4, 1)])
+        n = k + p
+        L = rnd.choice([1 << 20, (1 << 20) + 16 * rnd.randint(1, 400), 16 * rnd.randint(4096, 80000),
+                        rnd.randint(65536, 1 << 20)])
+        gap = rnd.choice([16, 48, 4096, 4096 * 3 + 16])
+        nbuf = 2 * n + 2
+        buf = np.random.default_rng(case).integers(0, 256, nbuf * (L + gap) + 8192, dtype=np.uint8)
+        start = (-buf.ctypes.data) % 4096 + 16 * rnd.randint(0, 255)
+        rows = _rows_in(buf[start:], nbuf, L, 0, gap)
+        code = _fz_code(fam, k, p, s)
+        data, par = rows[p:n], rows[:p]
+        ref = _fz_encode_ref(fam, k, p, s, [np.array(d) for d in data])
+        crc_ok = fam != "src" and rnd.random() < 0.5
+        if crc_ok:
+            run = [rnd.randrange(1 << 32) for _ in range(n)]
+            got = code.encodeBulkCrc(data, par, run)
+            assert got == [zlib.crc32(np.array(r).tobytes(), c) for r, c in zip(data + list(ref), run)], case
+        else:
+            code.encodeBulk(data, par)
+        paths.append(code.lastHostPath())
+        assert all(np.array_equal(par[o], ref[o]) for o in range(p)), (case, fam, k, p, L, paths[-1])
+        for r in rows[:p]:  # non-codeword reads: every decode coefficient counts
+            r[:] = np.frombuffer(rnd.randbytes(L), np.uint8)
+        erased, ntr, tr = _fz_pattern(fam, k, p, s, rnd)
+        src = [np.array(r) for r in rows[:n]]  # the rows before the decode
+        reads = [None if x in ntr else rows[x] for x in range(n)]
+        outs = rows[n:n + len(erased)]
+        if fam == "xor":
+            reads = [np.zeros(L, np.uint8) if r is None else r for r in reads]
+        ref_reads = [np.zeros(L, np.uint8) if (r is None and fam == "rs") else (None if r is None else np.array(r))
+                     for r in reads]
+        want = _fz_decode_ref(fam, k, p, s, ref_reads, erased, ntr, tr)
+        if crc_ok:
+            run = [rnd.randrange(1 << 32) for _ in erased]
+            got = code.decodeBulkCrc(reads, outs, erased, tr, ntr, run)
+            assert got == [zlib.crc32(w.tobytes(), c) for w, c in zip(want, run)], case
+        else:
+            code.decodeBulk(reads, outs, erased, tr, ntr)
+        paths.append(code.lastHostPath())
+        assert all(np.array_equal(outs[j], want[j]) for j in range(len(erased))), (case, fam, erased, ntr, paths[-1])
+        assert all(np.array_equal(rows[x], src[x]) for x in range(n)), case  # the reads are left as they were
+    # ragged lengths misalign every row after the first, and xor has no
+    # one-pass CRC: those calls take the staged path
+    assert paths.count("direct") >= len(paths) // 2, paths
