@@ -133,6 +133,32 @@ def test_direct_checksummed_calls(cuda):
     assert dcrc == [zlib.crc32(data[0].tobytes(), 7) & 0xFFFFFFFF]
 
 
+def test_direct_rows_of_one_array(cuda):
+    """Page-aligned rows back to back (one 2-D array, as the Python mirror's
+    callers hold a stripe): their page ranges touch and merge into one
+    registration; no head or tail columns."""
+    code = HipReedSolomonCode(K, P, zero_inputs_after_encode=False)
+    n = K + P
+    raw = np.random.default_rng(9).integers(0, 256, (n + 2) * L + 4096, dtype=np.uint8)
+    base = (-raw.ctypes.data) % 4096
+    rows = _rows_in(raw[base:], n + 2, L, 0, 0)
+    data, par = rows[P:n], rows[:P]
+    ref = C.encode_bulk(K, P, [np.array(d) for d in data])
+    run = [7 * i for i in range(n)]
+    crcs = code.encodeBulkCrc(data, par, run)
+    assert code.lastHostPath() == "direct"
+    assert all(np.array_equal(par[o], ref[o]) for o in range(P))
+    assert crcs == [zlib.crc32(np.array(r).tobytes(), c) for r, c in zip(data + list(ref), run)]
+    erased = [0, P + 3]
+    tr = sorted(C.locations_to_read(K, P, erased))
+    ntr = [x for x in range(n) if x not in tr]
+    want = [np.array(rows[e]) for e in erased]
+    outs = rows[n:n + 2]
+    code.decodeBulk([rows[i] if i in tr else None for i in range(n)], outs, erased, tr, ntr)
+    assert code.lastHostPath() == "direct"
+    assert all(np.array_equal(outs[j], want[j]) for j in range(2))
+
+
 def _page_rows(n, length, offset, rng):
     """n rows, each `offset` bytes past a page boundary of its own buffer."""
     rows = []
