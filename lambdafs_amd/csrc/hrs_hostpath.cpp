@@ -119,10 +119,9 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
 // tools/host_call_rate.cpp (profiles/r05/NOTES.md): encode 0.27 ms vs 0.36
 // staged, encode + CRC 0.29 vs 0.38, decode 0.25 vs 0.31.
 // Taken when zero copy is on, every row is 16-byte aligned, len >=
-// HRS_HOST_DIRECT_MIN (64 KiB: below it the copies cost less than the
-// registrations), the middle spans at least 32 KiB, a checksummed call's
-// middle kernel is one-pass (a two-pass CRC would read the cells across the
-// link twice), no other call of this process holds any of its pages
+// host_direct_min (128 KiB, 48 KiB for checksummed calls), the middle spans
+// at least 32 KiB, a checksummed call's middle kernel is one-pass (a
+// two-pass CRC would read the cells across the link twice), no other call of this process holds any of its pages
 // (PageClaims) and every range registers (pages the caller registered fail
 // it). Otherwise the call takes the staged path, with the same results.
 // HRS_HOST_DIRECT=0 turns it off (A/B runs; read per call).
@@ -131,13 +130,21 @@ bool host_direct_on() {
   return !(e && e[0] == '0');
 }
 
-size_t host_direct_min() {
-  static const size_t v = [] {
-    const char* e = getenv("HRS_HOST_DIRECT_MIN");
-    const long x = e ? atol(e) : -1;
-    return x >= 0 ? static_cast<size_t>(x) : static_cast<size_t>(64) << 10;
-  }();
-  return v;
+// Shortest row the direct path takes: HRS_HOST_DIRECT_MIN for plain calls
+// (default 128 KiB), HRS_HOST_DIRECT_MIN_CRC for checksummed ones (default
+// 48 KiB). Below them the staging copies cost no more than the registrations;
+// a checksummed call gains sooner, as its staged form pays a second launch
+// (profiles/r05/NOTES.md, cell-size sweep).
+size_t env_size(const char* name, size_t dflt) {
+  const char* e = getenv(name);
+  const long x = e ? atol(e) : -1;
+  return x >= 0 ? static_cast<size_t>(x) : dflt;
+}
+
+size_t host_direct_min(bool crc) {
+  static const size_t plain = env_size("HRS_HOST_DIRECT_MIN", static_cast<size_t>(128) << 10);
+  static const size_t with_crc = env_size("HRS_HOST_DIRECT_MIN_CRC", static_cast<size_t>(48) << 10);
+  return crc ? with_crc : plain;
 }
 
 // Runs the call over the caller's rows; false (nothing done, nothing left
@@ -145,7 +152,7 @@ size_t host_direct_min() {
 bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
                        uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc, int nlive,
                        hrs_status* st) {
-  if (!host_direct_on() || !zero_copy_on() || len < host_direct_min()) return false;
+  if (!host_direct_on() || !zero_copy_on() || len < host_direct_min(ncrc > 0)) return false;
   constexpr uintptr_t kPage = 4096;
   constexpr size_t kMinMid = 32u << 10;
   // the rows the call touches: live inputs, then outputs

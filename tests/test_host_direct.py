@@ -89,6 +89,26 @@ def test_fallbacks(cuda):
     _encode_check(code, small, out, "staged")
 
 
+def test_direct_thresholds(cuda):
+    """96 KiB rows: a plain call stays staged (below HRS_HOST_DIRECT_MIN,
+    128 KiB), a checksummed one goes direct (HRS_HOST_DIRECT_MIN_CRC, 48 KiB)."""
+    code = HipReedSolomonCode(K, P, zero_inputs_after_encode=False)
+    rng = np.random.default_rng(10)
+    Ls = 96 << 10
+    data = [rng.integers(0, 256, Ls, dtype=np.uint8) for _ in range(K)]
+    par = [np.zeros(Ls, np.uint8) for _ in range(P)]
+    ref = C.encode_bulk(K, P, [np.array(d) for d in data])
+    code.encodeBulk(data, par)
+    assert code.lastHostPath() == "staged"
+    assert all(np.array_equal(par[o], ref[o]) for o in range(P))
+    for x in par:
+        x[:] = 0
+    crcs = code.encodeBulkCrc(data, par)
+    assert code.lastHostPath() == "direct"
+    assert all(np.array_equal(par[o], ref[o]) for o in range(P))
+    assert crcs == [zlib.crc32(r.tobytes()) for r in data + list(ref)]
+
+
 def test_direct_decode_with_unread_rows(cuda):
     """decodeBulk 5-arg with the Decoder's arrays (Decoder.java:303-338): the
     not-to-read rows are None and never registered; the repaired rows are

@@ -2,24 +2,30 @@
 // shim calls per Encoder / Decoder round: HrsNative.encode / decode /
 // encodeCrc / decodeCrc -> hrs_encode / hrs_decode / hrs_encode_crc /
 // hrs_decode_crc), without the Python mirror's per-call argument marshalling:
-// one RS(10,4) stripe of 1 MiB pageable rows per call, the same rows every
-// call (Encoder.java:442 reuses its buffers), data shard 0 lost for decode.
-// Checks the first call of each kind against a copy of the data.
-// Usage: host_call_rate [calls]   (one JSON line)
+// one RS(k,p) stripe of L-byte pageable rows per call (default RS(10,4),
+// 1 MiB), the same rows every call (Encoder.java:442 reuses its buffers),
+// data shard 0 lost for decode. Checks the repaired row of each decode kind.
+// Usage: host_call_rate [calls] [L] [k] [p]   (one JSON line; "path" = the
+// host path hrs_last_host_path reports for the last encode)
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../include/hrs.h"
 
 int main(int argc, char** argv) {
   const int calls = argc > 1 ? atoi(argv[1]) : 200;
-  const int k = 10, p = 4, n = k + p;
-  const size_t L = 1 << 20;
+  const size_t L = argc > 2 ? static_cast<size_t>(atol(argv[2])) : static_cast<size_t>(1) << 20;
+  const int k = argc > 3 ? atoi(argv[3]) : 10, p = argc > 4 ? atoi(argv[4]) : 4, n = k + p;
+  if (calls < 1 || L < 8 || k < 1 || p < 1 || n > 255) {
+    fprintf(stderr, "usage: host_call_rate [calls] [L >= 8] [k] [p]\n");
+    return 1;
+  }
   hrs_opts o{};
   o.device = 0;
   hrs_codec* c = nullptr;
@@ -59,6 +65,7 @@ int main(int argc, char** argv) {
   };
   bool ok = true;
   const double enc = time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; });
+  const std::string path = hrs_last_host_path(c);
   const double dec = time_it([&] {
     ok &= hrs_decode(c, reads.data(), &lostp, erased, 1, to_read, nr, ntr.data(), static_cast<int>(ntr.size()), L) ==
           HRS_OK;
@@ -72,11 +79,11 @@ int main(int argc, char** argv) {
   ok &= memcmp(lost.data(), rows[p].data(), L) == 0;
   const double gib = static_cast<double>(k) * L / (1u << 30);
   const char* zc = getenv("HRS_ZEROCOPY");
-  printf("{\"path\": \"C ABI synchronous host-buffer calls, RS(10,4) 1 MiB pageable rows, 1 stripe per call\", "
-         "\"zero_copy\": %s, \"calls\": %d, \"encode_ms\": %.4f, \"encode_GiBps_user\": %.2f, \"decode_ms\": %.4f, "
+  printf("{\"what\": \"C ABI synchronous host-buffer calls, one RS(k,p) stripe of pageable rows per call\", "
+         "\"k\": %d, \"p\": %d, \"L\": %zu, \"path\": \"%s\", \"zero_copy\": %s, \"calls\": %d, \"encode_ms\": %.4f, \"encode_GiBps_user\": %.2f, \"decode_ms\": %.4f, "
          "\"decode_GiBps_user\": %.2f, \"encode_crc_ms\": %.4f, \"encode_crc_GiBps_user\": %.2f, "
          "\"decode_crc_ms\": %.4f, \"decode_crc_GiBps_user\": %.2f, \"ok\": %s}\n",
-         (zc && zc[0] == '0') ? "false" : "true", calls, enc, gib / (enc * 1e-3), dec, gib / (dec * 1e-3), encc,
+         k, p, L, path.c_str(), (zc && zc[0] == '0') ? "false" : "true", calls, enc, gib / (enc * 1e-3), dec, gib / (dec * 1e-3), encc,
          gib / (encc * 1e-3), decc, gib / (decc * 1e-3), ok ? "true" : "false");
   hrs_destroy(c);
   return ok ? 0 : 1;
