@@ -346,7 +346,7 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     over 8), a seeded random PAIR of lost locations per stripe (keyed by the
     global stripe index), the stripes in pinned host memory; only each
     stripe's 12 survivors cross PCIe H2D, only the 2 repaired cells come back.
-    Also the same path staged from pageable memory, and the host batch encode
+    Also the same call on pageable memory, and the host batch encode
     (hrs_encode_batch_host: 12 data cells H2D, 4 parity cells D2H). The
     repaired cells are hashed per 256-stripe block and compared with the
     oracle's digests (golden["config5"]).
@@ -388,10 +388,12 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     idx = np.arange(S)[:, None]
     dec_ok = bool(np.array_equal(outn, stn[idx, er]))
     mine = SD.stripe_digests(lambda a, b: outn[a:b], S, g0)
-    # pageable host memory: the same call stages through pinned slots
+    # pageable host memory: the call registers the batch's whole pages for
+    # its duration ("direct"; HRS_HOST_DIRECT=0: staged through pinned slots)
     pg = np.array(stn)
     pout = np.zeros((S, 2, L), np.uint8)
     pg_ms = timed(lambda: device.decode_batch_host(code, pg, er, pout))
+    pg_path = code.lastHostPath()
     pg_ok = bool(np.array_equal(pout, pg[idx, er]))
     del pg, pout
     # the link's own rate for the same survivor bytes: one pinned H2D copy
@@ -422,6 +424,7 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
         "h2d_peak_how": "one pinned-host to device copy of the same 12 * 256 KiB * S survivor bytes",
         "decode_pageable_ms": stats(pg_ms),
         "decode_pageable_GiBps_user": rate(t_pg, user),
+        "decode_pageable_path": pg_path,
         "encode_ms": stats(enc_ms),
         "encode_GiBps_user": rate(t_enc, user),
         "encode_pcie_GBps": round((k + p) * L * S * world / 1e9 / (t_enc * 1e-3), 2),

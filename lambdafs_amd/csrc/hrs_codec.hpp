@@ -165,6 +165,35 @@ unsigned zero_copy_blocks();
 // false for pageable memory.
 bool host_device_ptr(const void* p, uint8_t** dp);
 
+// ---- pageable memory made visible to the GPU for one call (hrs_hostpath.cpp)
+// HRS_HOST_DIRECT=0 turns it off (read per call); host_direct_min: shortest
+// row (or batch span) worth it, plain / checksummed calls.
+bool host_direct_on();
+size_t host_direct_min(bool crc);
+// Host page ranges [first, second) registered with HIP (hipHostRegister,
+// mapped) for the duration of one call. The ranges are sorted and merged
+// (overlapping or touching), claimed process-wide (PageClaims: HIP would
+// accept a page registered twice and then drop it under the other call) and
+// registered. ok() is false, with nothing held, when a claim or registration
+// fails or a device address differs from its host address (zero copy needs
+// them equal). release() (or the destructor) unregisters and drops the
+// claims; every stream that reads the pages must have drained by then.
+class RegisteredPages {
+ public:
+  explicit RegisteredPages(std::vector<std::pair<uintptr_t, uintptr_t>> ranges);
+  ~RegisteredPages() { release(); }
+  RegisteredPages(const RegisteredPages&) = delete;
+  RegisteredPages& operator=(const RegisteredPages&) = delete;
+  bool ok() const { return ok_; }
+  void release();
+
+ private:
+  std::vector<std::pair<uintptr_t, uintptr_t>> rg_;
+  std::vector<uintptr_t> held_;
+  bool claimed_ = false;
+  bool ok_ = false;
+};
+
 // The compile-time encode kernels hold the hops RS generator (rs) or the
 // ISA-L Cauchy rows (nrs) of a (k, p) shape; only those families' G may take
 // them. SRC's G (XOR groups over RS(k, r)) and XOR's all-ones row may not.

@@ -101,10 +101,10 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
 // first copy-in and the last copy-out on the critical path). Instead, the
 // caller's rows are made visible to the GPU for the call and the zero-copy
 // kernel reads the inputs and writes the outputs in place:
-//   - only pages that lie wholly inside a row are registered (hipHostRegister,
-//     mapped; ~0.9 us per row, ~0.4 us to unregister), so no page holding anyone else's bytes is
-//     ever registered (a pageable HIP copy by other code that touched such a
-//     page during the call would otherwise fail);
+//   - only pages that lie wholly inside a row are registered (RegisteredPages;
+//     ~0.9 us per row, ~0.4 us to unregister), so no page holding anyone
+//     else's bytes is ever registered (a pageable HIP copy by other code that
+//     touched such a page during the call would otherwise fail);
 //   - the columns every row has inside its whole pages, [c0, c1) with c1 - c0
 //     a multiple of 2 KiB, run over the caller's rows; the head [0, c0) and
 //     the tail [c1, len) (each under 4 KiB + 2 KiB) are copied through the
@@ -121,9 +121,9 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
 // Taken when zero copy is on, every row is 16-byte aligned, len >=
 // host_direct_min (128 KiB, 48 KiB for checksummed calls), the middle spans
 // at least 32 KiB, a checksummed call's middle kernel is one-pass (a
-// two-pass CRC would read the cells across the link twice), no other call of this process holds any of its pages
-// (PageClaims) and every range registers (pages the caller registered fail
-// it). Otherwise the call takes the staged path, with the same results.
+// two-pass CRC would read the cells across the link twice), no other call of
+// this process holds any of its pages (PageClaims) and every range registers
+// (pages the caller registered fail it). Otherwise the call takes the staged path, with the same results.
 // HRS_HOST_DIRECT=0 turns it off (A/B runs; read per call).
 bool host_direct_on() {
   const char* e = getenv("HRS_HOST_DIRECT");
@@ -145,6 +145,44 @@ size_t host_direct_min(bool crc) {
   static const size_t plain = env_size("HRS_HOST_DIRECT_MIN", static_cast<size_t>(128) << 10);
   static const size_t with_crc = env_size("HRS_HOST_DIRECT_MIN_CRC", static_cast<size_t>(48) << 10);
   return crc ? with_crc : plain;
+}
+
+RegisteredPages::RegisteredPages(std::vector<std::pair<uintptr_t, uintptr_t>> ranges) : rg_(std::move(ranges)) {
+  std::sort(rg_.begin(), rg_.end());
+  size_t w = 0;  // merge overlapping and touching ranges: each page is registered once
+  for (size_t r = 1; r < rg_.size(); ++r) {
+    if (rg_[r].first <= rg_[w].second)
+      rg_[w].second = std::max(rg_[w].second, rg_[r].second);
+    else
+      rg_[++w] = rg_[r];
+  }
+  rg_.resize(rg_.empty() ? 0 : w + 1);
+  if (rg_.empty() || !hrs::PageClaims::instance().claim(rg_)) return;  // another call holds some of these pages
+  claimed_ = true;
+  for (const auto& r : rg_) {
+    if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first, hipHostRegisterMapped) != hipSuccess) {
+      (void)hipGetLastError();  // already registered (by the caller), or not registrable
+      release();
+      return;
+    }
+    held_.push_back(r.first);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(r.first), 0) != hipSuccess ||
+        d != reinterpret_cast<void*>(r.first)) {
+      (void)hipGetLastError();
+      release();
+      return;
+    }
+  }
+  ok_ = true;
+}
+
+void RegisteredPages::release() {
+  for (uintptr_t a : held_) (void)hipHostUnregister(reinterpret_cast<void*>(a));
+  held_.clear();
+  if (claimed_) hrs::PageClaims::instance().release(rg_);
+  claimed_ = false;
+  ok_ = false;
 }
 
 // Runs the call over the caller's rows; false (nothing done, nothing left
@@ -175,18 +213,6 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
   // registration ranges: the whole pages of each row under [c0, c1)
   std::vector<std::pair<uintptr_t, uintptr_t>> rg;
   for (uintptr_t a : rows) rg.push_back({(a + c0) & ~(kPage - 1), (a + c1 + kPage - 1) & ~(kPage - 1)});
-  std::sort(rg.begin(), rg.end());
-  // one range per row; overlapping ranges (a row passed twice) and touching
-  // ones (page-aligned rows back to back, e.g. one 2-D array) merge, so such
-  // a call registers once (~1.3 us per registration and unregistration)
-  size_t w = 0;
-  for (size_t r = 1; r < rg.size(); ++r) {
-    if (rg[r].first <= rg[w].second)
-      rg[w].second = std::max(rg[w].second, rg[r].second);
-    else
-      rg[++w] = rg[r];
-  }
-  rg.resize(rg.empty() ? 0 : w + 1);
   // staging for the head and tail columns (pinned, device-mapped), their CRC
   // words, and the raw window-CRC scratch: all before any page is registered.
   // The head and the tail run as ONE launch of two "stripes" (stripe 0 the
@@ -220,27 +246,8 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     *st = s0;
     return true;
   }
-  if (!hrs::PageClaims::instance().claim(rg)) return false;  // another call holds some of these pages
-  std::vector<uintptr_t> held;
-  auto release = [&] {
-    for (uintptr_t a : held) (void)hipHostUnregister(reinterpret_cast<void*>(a));
-    hrs::PageClaims::instance().release(rg);
-  };
-  for (const auto& r : rg) {
-    if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first, hipHostRegisterMapped) != hipSuccess) {
-      (void)hipGetLastError();  // already registered (by the caller or another call), or not registrable
-      release();
-      return false;
-    }
-    held.push_back(r.first);
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(r.first), 0) != hipSuccess ||
-        d != reinterpret_cast<void*>(r.first)) {  // zero copy needs the device address to be the host address
-      (void)hipGetLastError();
-      release();
-      return false;
-    }
-  }
+  RegisteredPages reg(std::move(rg));  // merged: a row passed twice, or rows back to back, register once
+  if (!reg.ok()) return false;
   hrs_codec::HostSlot& h = c->host[0];
   const hipStream_t s = h.stream, s_ht = c->host[1].stream;
   c->last_host_path = "direct";
@@ -298,7 +305,7 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     e = hipStreamSynchronize(s_ht);
     if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
   }
-  release();
+  reg.release();
   if (rs == HRS_OK) {
     for (int o = 0; o < nout; ++o) {
       const uint8_t* hr = h.pin + W * (nlive + o);

@@ -21,17 +21,23 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "duplex"])
+@pytest.fixture(autouse=True, params=["zero_copy", "staged", "copy_engine", "duplex"])
 def transfer_mode(request, monkeypatch):
     """Every test runs every way the host batches can move bytes: zero copy
-    (the default: kernels read and write pinned host memory across the link),
+    (the default: kernels read and write pinned host memory across the link;
+    pageable batches have their pages registered for the call, the "direct"
+    path, with the few stripes at either end that reach into partial pages
+    staged), the staged zero-copy path for pageable batches (HRS_HOST_DIRECT=0),
     the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H on each
     slot's stream), and the copy engine with the directions split over the
     shared copy-in / copy-out streams (HRS_HBATCH_DUPLEX=1: in_done /
     comp_done / done events chain the three streams per slot)."""
     monkeypatch.delenv("HRS_HBATCH_DUPLEX", raising=False)
-    if request.param == "zero_copy":
+    monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
+    if request.param in ("zero_copy", "staged"):
         monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+        if request.param == "staged":
+            monkeypatch.setenv("HRS_HOST_DIRECT", "0")
     else:
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
         if request.param == "duplex":
@@ -217,3 +223,70 @@ def test_host_batches_on_interior_pinned_views(cuda):
     device.decode_batch_host(code, st, er, out)
     for s in range(S):
         assert np.array_equal(out[s], st[s, er[s]]), s
+
+
+@pytest.mark.parametrize("offset", [0, 16, 4000])
+def test_pageable_batches_path_and_parity(cuda, transfer_mode, offset):
+    """Pageable batches that start `offset` bytes past a page boundary (0: the
+    stripes fill whole pages; otherwise the first and last stripes reach into
+    partial pages and are staged after the registered middle). The path each
+    mode takes (hrs_last_host_path), parity vs the oracle for every stripe,
+    and every repaired cell; pinned buffers report "pinned"."""
+    torch = cuda
+    k, p, S, L = 10, 4, 12, 64 << 10
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=0)
+    rng = np.random.default_rng(offset + 1)
+    raw = np.empty(S * n * L + offset + 8192, np.uint8)
+    base = (-raw.ctypes.data) % 4096 + offset
+    st = raw[base:base + S * n * L].reshape(S, n, L)
+    st[:, p:] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    st[:, :p] = 0xA5
+    oraw = np.empty(S * 2 * L + offset + 8192, np.uint8)
+    obase = (-oraw.ctypes.data) % 4096 + offset
+    out = oraw[obase:obase + S * 2 * L].reshape(S, 2, L)
+    want = {"zero_copy": "direct", "staged": "staged", "copy_engine": "copy_engine", "duplex": "copy_engine"}
+    device.encode_batch_host(code, st)
+    assert code.lastHostPath() == want[transfer_mode]
+    for s in range(S):
+        ref = C.encode_bulk(k, p, [st[s, p + c].copy() for c in range(k)])
+        assert all((st[s, r] == ref[r]).all() for r in range(p)), s
+    er = _patterns(random.Random(offset), S, n, 2, lambda s: 2)
+    out[:] = 0xEE
+    device.decode_batch_host(code, st, er, out)
+    assert code.lastHostPath() == want[transfer_mode]
+    for s in range(S):
+        assert np.array_equal(out[s], st[s, er[s]]), s
+    pin = _alloc(torch, (S, n, L), True)
+    pin[:] = st
+    pout = _alloc(torch, (S, 2, L), True)
+    device.decode_batch_host(code, pin, er, pout)
+    assert code.lastHostPath() == ("pinned" if transfer_mode in ("zero_copy", "staged") else "copy_engine")
+    assert np.array_equal(pout, out)
+
+
+def test_pageable_multi_batch_direct(cuda, transfer_mode):
+    """hrs_decode_batch_host_multi over the device set {0, 0} on pageable
+    memory: each member registers the whole pages of its own stripe range
+    (the page the two ranges share belongs to neither and its stripes are
+    staged); every repaired cell and every parity row checked."""
+    k, p, S, L = 12, 4, 16, 64 << 10
+    n = k + p
+    codes = [HipReedSolomonCode(k, p, device=0) for _ in range(2)]
+    rng = np.random.default_rng(21)
+    raw = np.empty(S * n * L + 8192 + 48, np.uint8)
+    base = (-raw.ctypes.data) % 4096 + 48
+    st = raw[base:base + S * n * L].reshape(S, n, L)
+    st[:, p:] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    device.encode_batch_host_multi(codes, st)
+    for s in range(S):
+        ref = C.encode_bulk(k, p, [st[s, p + c].copy() for c in range(k)])
+        assert all((st[s, r] == ref[r]).all() for r in range(p)), s
+    er = _patterns(random.Random(2), S, n, 2, lambda s: 1 + s % 2)
+    out = np.full((S, 2, L), 0xEE, np.uint8)
+    device.decode_batch_host_multi(codes, st, er, out)
+    for s in range(S):
+        lost = [int(x) for x in er[s] if x >= 0]
+        assert np.array_equal(out[s, :len(lost)], st[s, lost]), (s, lost)
+    if transfer_mode == "zero_copy":
+        assert [c.lastHostPath() for c in codes] == ["direct", "direct"]
