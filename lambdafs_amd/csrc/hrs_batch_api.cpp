@@ -586,6 +586,13 @@ using namespace hrs::api;
 
 namespace {
 
+// hrs_last_host_path of a batch that was not registered for the call.
+const char* batch_path(const void* in, const void* out) {
+  uint8_t* d = nullptr;
+  if (!zero_copy_on()) return "copy_engine";
+  return host_device_ptr(in, &d) && host_device_ptr(out, &d) ? "pinned" : "staged";
+}
+
 // Pageable host batches straight over the caller's memory (round 5, as the
 // synchronous calls: hrs_hostpath.cpp host_apply_direct). The whole pages
 // inside the batch's spans (stripes, and the outputs of a decode) are
@@ -597,37 +604,6 @@ namespace {
 // staged. Taken when zero copy is on, HRS_HOST_DIRECT is not 0, the buffers
 // are pageable, the inner stripes span at least host_direct_min and every
 // claim and registration succeeds; otherwise the whole batch is staged.
-struct InnerStripes {
-  size_t lo = 0, hi = 0;  // stripes [lo, hi) lie inside the whole pages [p0, p1)
-  uintptr_t p0 = 0, p1 = 0;
-};
-
-// Stripes of a strided array (stripe s at base + s * stride, `ext` bytes
-// long) that lie inside the whole pages of the array's span.
-InnerStripes inner_stripes(const void* base, size_t stride, size_t ext, size_t nstripes) {
-  constexpr uintptr_t kPage = 4096;
-  InnerStripes r;
-  if (nstripes == 0 || ext == 0 || (nstripes > 1 && stride < ext)) return r;  // overlapping stripes: no
-  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-  const uintptr_t end = b + (nstripes - 1) * stride + ext;
-  r.p0 = (b + kPage - 1) & ~(kPage - 1);
-  r.p1 = end & ~(kPage - 1);
-  if (r.p1 <= r.p0) return r;
-  const size_t st = std::max<size_t>(stride, 1);
-  r.lo = (r.p0 - b + st - 1) / st;
-  if (r.p1 < b + ext) return r;
-  r.hi = std::min<size_t>(nstripes, (r.p1 - b - ext) / st + 1);
-  if (r.hi < r.lo) r.hi = r.lo;
-  return r;
-}
-
-// hrs_last_host_path of a batch that was not registered for the call.
-const char* batch_path(const void* in, const void* out) {
-  uint8_t* d = nullptr;
-  if (!zero_copy_on()) return "copy_engine";
-  return host_device_ptr(in, &d) && host_device_ptr(out, &d) ? "pinned" : "staged";
-}
-
 bool batch_direct_candidate(const void* p) {
   uint8_t* d = nullptr;
   return host_direct_on() && zero_copy_on() && !host_device_ptr(p, &d);
@@ -800,9 +776,9 @@ hrs_status hrs_decode_batch_host(hrs_codec* c, const uint8_t* stripes, size_t ro
   }
   DeviceGuard g(c->device);  // a registration maps the pages for the codec's device
   if (g.ok && batch_direct_candidate(stripes) && batch_direct_candidate(out)) {
-    const InnerStripes a = inner_stripes(stripes, stripe_stride, (c->n - 1) * row_stride + len, nstripes);
-    const InnerStripes b =
-        inner_stripes(out, out_stripe_stride, static_cast<size_t>(max_erased - 1) * out_row_stride + len, nstripes);
+    const hrs::InnerStripes a = hrs::inner_stripes(stripes, stripe_stride, (c->n - 1) * row_stride + len, nstripes);
+    const size_t out_ext = static_cast<size_t>(max_erased - 1) * out_row_stride + len;
+    const hrs::InnerStripes b = hrs::inner_stripes(out, out_stripe_stride, out_ext, nstripes);
     const size_t lo = std::max(a.lo, b.lo), hi = std::min(a.hi, b.hi);
     if (hi > lo && (hi - lo) * stripe_stride >= host_direct_min(false)) {
       RegisteredPages reg({{a.p0, a.p1}, {b.p0, b.p1}});
@@ -837,7 +813,7 @@ hrs_status hrs_encode_batch_host(hrs_codec* c, uint8_t* stripes, size_t row_stri
   if (nstripes == 0 || len == 0) return HRS_OK;
   DeviceGuard g(c->device);
   if (g.ok && batch_direct_candidate(stripes)) {
-    const InnerStripes a = inner_stripes(stripes, stripe_stride, (c->n - 1) * row_stride + len, nstripes);
+    const hrs::InnerStripes a = hrs::inner_stripes(stripes, stripe_stride, (c->n - 1) * row_stride + len, nstripes);
     if (a.hi > a.lo && (a.hi - a.lo) * stripe_stride >= host_direct_min(false)) {
       RegisteredPages reg({{a.p0, a.p1}});
       if (reg.ok()) {

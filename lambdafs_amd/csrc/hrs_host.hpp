@@ -13,8 +13,10 @@
 // the MI355X hosts whatever the worker count: tools/pool_probe.cpp). A call
 // returns once all its pieces are copied and no worker still holds its batch.
 //
-// Also the process-wide claims on host page ranges the synchronous calls
-// register with HIP for their duration (PageClaims, hrs_hostpath.cpp).
+// Also the process-wide claims on host page ranges the synchronous calls and
+// pageable host batches register with HIP for their duration (PageClaims,
+// hrs_hostpath.cpp RegisteredPages), and the stripes of a strided batch that
+// lie inside whole pages (inner_stripes, hrs_batch_api.cpp).
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -214,5 +216,31 @@ class PageClaims {
   std::mutex mu_;
   std::map<uintptr_t, uintptr_t> held_;  // start -> end, disjoint
 };
+
+struct InnerStripes {
+  size_t lo = 0, hi = 0;  // stripes [lo, hi) lie inside the whole pages [p0, p1)
+  uintptr_t p0 = 0, p1 = 0;
+};
+
+// Stripes of a strided array (stripe s at base + s * stride, `ext` bytes
+// long) that lie inside the whole pages [p0, p1) of the array's span: a
+// contiguous range [lo, hi), empty (hi <= lo) when none does or the stripes
+// overlap (stride < ext).
+inline InnerStripes inner_stripes(const void* base, size_t stride, size_t ext, size_t nstripes) {
+  constexpr uintptr_t kPage = 4096;
+  InnerStripes r;
+  if (nstripes == 0 || ext == 0 || (nstripes > 1 && stride < ext)) return r;  // overlapping stripes: no
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+  const uintptr_t end = b + (nstripes - 1) * stride + ext;
+  r.p0 = (b + kPage - 1) & ~(kPage - 1);
+  r.p1 = end & ~(kPage - 1);
+  if (r.p1 <= r.p0) return r;
+  const size_t st = nstripes > 1 ? stride : ext;  // one stripe: its stride is never used
+  r.lo = (r.p0 - b + st - 1) / st;
+  if (r.p1 < b + ext) return r;
+  r.hi = std::min<size_t>(nstripes, (r.p1 - b - ext) / st + 1);
+  if (r.hi < r.lo) r.hi = r.lo;
+  return r;
+}
 
 }  // namespace hrs

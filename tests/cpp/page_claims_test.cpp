@@ -2,7 +2,10 @@
 // the synchronous direct calls register with HIP (hrs_hostpath.cpp). Checks the
 // overlap rules single-threaded, then N threads claiming random ranges of a
 // small page space at once: a claimed page is never claimed by a second
-// holder, and every claim is released. CPU only (also under `make tsan`).
+// holder, and every claim is released. Then hrs::inner_stripes (the stripes
+// of a pageable host batch that lie inside whole pages, hrs_batch_api.cpp)
+// against a brute-force scan over random layouts. CPU only (also under
+// `make tsan`).
 // Usage: page_claims_test [threads] [iterations]   (one JSON line)
 #include <atomic>
 #include <cstdio>
@@ -75,9 +78,32 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   bad += !pc.claim({R(0, npages)});  // every claim was released
   pc.release({R(0, npages)});
+  // inner_stripes vs brute force: stripe s is inside iff its first byte is at
+  // or past the first whole page and its last byte before the span's last
+  // partial page; the inside stripes must be exactly [lo, hi)
+  std::mt19937 rng(99);
+  int inner_bad = 0;
+  for (int it = 0; it < 20000; ++it) {
+    const uintptr_t b = base + rng() % (3 * P);
+    const size_t ext = 1 + rng() % (5 * P);
+    const size_t ns = rng() % 12;
+    const size_t stride = (rng() % 8 == 0) ? rng() % (ext + 1) : ext + (rng() % 3) * (rng() % (2 * P));
+    const hrs::InnerStripes r = hrs::inner_stripes(reinterpret_cast<const void*>(b), stride, ext, ns);
+    const bool overl = ns > 1 && stride < ext;
+    const uintptr_t p0 = (b + P - 1) / P * P, p1 = ns ? (b + (ns - 1) * stride + ext) / P * P : 0;
+    for (size_t s = 0; s < ns; ++s) {
+      const bool in = !overl && ns && b + s * stride >= p0 && b + s * stride + ext <= p1;
+      const bool said = s >= r.lo && s < r.hi;
+      if (in != said) inner_bad++;
+      if (said && (r.p0 != p0 || r.p1 != p1)) inner_bad++;
+    }
+    if (r.hi > ns) inner_bad++;
+  }
+  bad += inner_bad;
   const bool ok = bad == 0 && violations == 0;
-  printf("{\"threads\": %d, \"iterations\": %d, \"rule_failures\": %d, \"violations\": %d, \"granted\": %ld, "
-         "\"refused\": %ld, \"ok\": %s}\n",
-         nthreads, iters, bad, violations.load(), granted.load(), refused.load(), ok ? "true" : "false");
+  printf("{\"threads\": %d, \"iterations\": %d, \"inner_stripes_failures\": %d, \"rule_failures\": %d, "
+         "\"violations\": %d, \"granted\": %ld, \"refused\": %ld, \"ok\": %s}\n",
+         nthreads, iters, inner_bad, bad - inner_bad, violations.load(), granted.load(), refused.load(),
+         ok ? "true" : "false");
   return ok ? 0 : 1;
 }
