@@ -259,6 +259,74 @@ def host_calls(local, calls=100):
     return res
 
 
+def sync_threads(local, codecs=(1, 2, 4), calls=48):
+    """The unmodified Encoder at raid.encoder.parallelism = T (Encoder.java:
+    77-80: T Encoders, one codec and one thread each, every round a
+    synchronous encodeBulk, :442): T host threads each calling hrs_encode on
+    their own RS(10,4) stripe of 1 MiB pageable rows, back to back, on one
+    GPU. Per T: the aggregate user-data rate, the per-call time and the host
+    path the calls took. Every thread's last parity is checked against the
+    first thread's first call (same data rows)."""
+    import threading
+    from lambdafs_amd import _lib
+    from lambdafs_amd._lib import ptr_array
+    k, p, L = 10, 4, 1 << 20
+    lib = _lib.lib()
+    rng = np.random.default_rng(0x5EED000C)
+    data0 = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    workers = []
+    for _ in range(max(codecs)):
+        code = HipReedSolomonCode(k, p, device=local, zero_inputs_after_encode=False)
+        data = [d.copy() for d in data0]  # each thread its own rows, as each Encoder reads its own
+        outs = [np.zeros(L, np.uint8) for _ in range(p)]
+        workers.append({"code": code, "h": code._handle(), "data": data, "outs": outs,
+                        "ins": ptr_array([d.ctypes.data for d in data]),
+                        "outp": ptr_array([o.ctypes.data for o in outs])})
+    w0 = workers[0]
+    w0["code"]._check(lib.hrs_encode(w0["h"], w0["ins"], w0["outp"], L))
+    ref = [o.copy() for o in w0["outs"]]
+    res = {"what": "T threads x one RS(10,4) codec each, back-to-back synchronous hrs_encode calls on one 1 MiB "
+                   "pageable stripe per call (the unmodified Encoder at raid.encoder.parallelism = T), one GPU",
+           "calls_per_thread": calls}
+
+    def run(T):
+        errs, per = [], []
+        lock = threading.Lock()
+
+        def body(w):
+            ms = []
+            try:
+                for _ in range(calls):
+                    t0 = time.perf_counter()
+                    w["code"]._check(lib.hrs_encode(w["h"], w["ins"], w["outp"], L))
+                    ms.append((time.perf_counter() - t0) * 1e3)
+            except Exception as e:  # noqa: BLE001 - reported after the join
+                errs.append(e)
+            with lock:
+                per.extend(ms)
+
+        ths = [threading.Thread(target=body, args=(w,)) for w in workers[:T]]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        wall = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        if not all(np.array_equal(a, b) for w in workers[:T] for a, b in zip(w["outs"], ref)):
+            raise RuntimeError("concurrent synchronous encodes differ")
+        return {"threads": T, "wall_ms": round(wall * 1e3, 2),
+                "GiBps_user": round(T * calls * k * L / GiB / wall, 2),
+                "call_ms": {"median": round(float(np.median(per)), 4), "p90": round(float(np.percentile(per, 90)), 4)},
+                "paths": sorted({w["code"].lastHostPath() for w in workers[:T]})}
+
+    run(max(codecs))  # warm every codec's staging and streams
+    res["by_threads"] = [run(T) for T in codecs]
+    res["bit_exact"] = True
+    return res
+
+
 def async_rounds(local, codecs=4, depths=(1, 2, 4), rounds=48):
     """The asynchronous drop-in under Encoder-shaped traffic (VERDICT r4 item
     5; HipReedSolomonCode.encodeBulkAsync / collect, Encoder.java:421-453):
@@ -1069,6 +1137,7 @@ def run(args):
         }
         res["host_calls"] = None if args.no_host_calls else host_calls(local)
         res["async_rounds"] = None if args.no_host_calls else async_rounds(local)
+        res["sync_threads"] = None if args.no_host_calls else sync_threads(local)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, p, L, args.cpu_stripes)
             res["cpu_baseline_1thread"] = cpu_baseline(k, p, L, 40, threads=1)
