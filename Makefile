@@ -130,7 +130,7 @@ SAN      := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-om
 HSAN     := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
             -Xarch_host -fno-omit-frame-pointer
 ASAN_BIN := $(ASAN_DIR)/host_logic $(ASAN_DIR)/jni_harness $(ASAN_DIR)/codec_harness
-ASAN_LOG := profiles/r04/asan
+ASAN_LOG := profiles/r05/asan
 
 ASAN_API := $(patsubst %,$(ASAN_DIR)/%.o,$(API_SRC))
 $(ASAN_API): $(ASAN_DIR)/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
