@@ -7,7 +7,13 @@
   covers 1-2 erasures; here all 4 levels);
 - wide codes: RS(100,10) and the maximum RS(245,10) (k + p = 255 < 256,
   ReedSolomonCode.java:57), exercising the host's input/output chunking;
-- decodes with more than 8 erased rows (output chunking).
+- decodes with more than 8 erased rows (output chunking);
+- every 1..p erasure pattern of each BASELINE shape (RS(3,2), RS(6,3),
+  RS(10,4), RS(12,4): 30 / 129 / 1,470 / 2,516 patterns) as ONE heterogeneous
+  batch launch (hrs_decode_batch_dev, a different pattern per stripe) on
+  NON-codeword stripes, every stripe vs the oracle's per-byte decodeBulk
+  5-arg (ReedSolomonCode.java:191-211) with the Decoder's zero rows for the
+  unread locations (StripeReader.java:106-124).
 """
 import itertools
 import random
@@ -90,3 +96,28 @@ def test_wide_codes_encode_and_decode(cuda, k, p):
         out = torch.empty((S, e, L), dtype=torch.uint8, device="cuda")
         device.decode_stripes(code, st, erased, ntr, out)
         assert torch.equal(out, st[:, erased, :]), (k, p, erased)
+
+
+@pytest.mark.parametrize("k,p", [(3, 2), (6, 3), (10, 4), (12, 4)])
+def test_every_pattern_in_one_batch_vs_oracle(cuda, k, p):
+    torch = cuda
+    n, L = k + p, 2048 + 48  # one fused window and a ragged tail
+    pats = [list(e) for m in range(1, p + 1) for e in itertools.combinations(range(n), m)]
+    S = len(pats)
+    er = np.full((S, p), -1, dtype=np.int32)
+    for s, e in enumerate(pats):
+        er[s, :len(e)] = e
+    g = torch.Generator(device="cuda")
+    g.manual_seed(k * 100 + p)
+    st = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device="cuda", generator=g)  # non-codewords
+    out = torch.full((S, p, L), 0xEE, dtype=torch.uint8, device="cuda")
+    code = HipReedSolomonCode(k, p)
+    device.decode_batch(code, st, er, out)
+    host, got = st.cpu().numpy(), out.cpu().numpy()
+    for s, erased in enumerate(pats):
+        to_read = sorted(C.locations_to_read(k, p, erased))
+        ntr = [x for x in range(n) if x not in to_read or x in erased]
+        reads = [np.zeros(L, np.uint8) if x in ntr else host[s, x] for x in range(n)]
+        ref = C.decode_bulk5(k, p, reads, erased, to_read, ntr)
+        for j in range(len(erased)):
+            assert np.array_equal(got[s, j], ref[j]), (erased, j)
