@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -187,6 +188,25 @@ void RegisteredPages::release() {
 
 // Runs the call over the caller's rows; false (nothing done, nothing left
 // registered) when the call must take the staged path. *st: its status.
+// One direct call at a time per process: a call that finds another one in
+// flight takes the staged path. One direct caller already fills the host
+// link; beside it, the staged callers' host copies overlap its link time,
+// where overlapping direct calls only split the link (and churn
+// registrations): 4 concurrent Encoders 38.8-39.6 GiB/s of user data this
+// way, 31.9-34.9 with direct calls overlapping, 35.3-38.1 all staged
+// (profiles/r05/NOTES.md). HRS_HOST_DIRECT_EXCL=0 lets them overlap (A/B
+// runs; read per call).
+std::atomic<int> g_direct_inflight{0};
+struct DirectTurn {
+  bool ok = true;
+  DirectTurn() {
+    const char* e = getenv("HRS_HOST_DIRECT_EXCL");
+    const int before = g_direct_inflight.fetch_add(1);
+    if (!(e && e[0] == '0') && before > 0) ok = false;
+  }
+  ~DirectTurn() { g_direct_inflight.fetch_sub(1); }
+};
+
 bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
                        uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc, int nlive,
                        hrs_status* st) {
@@ -246,6 +266,8 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     *st = s0;
     return true;
   }
+  DirectTurn turn;
+  if (!turn.ok) return false;
   RegisteredPages reg(std::move(rg));  // merged: a row passed twice, or rows back to back, register once
   if (!reg.ok()) return false;
   hrs_codec::HostSlot& h = c->host[0];

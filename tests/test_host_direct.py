@@ -223,11 +223,24 @@ def test_direct_head_tail_shapes(cuda, offset, length):
     assert dcrc == [zlib.crc32(stripe[e].tobytes(), 5 + j) & 0xFFFFFFFF for j, e in enumerate(erased)]
 
 
+@pytest.fixture(params=["exclusive", "overlapping"])
+def direct_turns(request, monkeypatch):
+    """Concurrent callers: by default one direct call at a time (the others
+    staged); HRS_HOST_DIRECT_EXCL=0 lets direct calls overlap, which is where
+    the page claims (PageClaims) keep two calls off the same pages."""
+    if request.param == "overlapping":
+        monkeypatch.setenv("HRS_HOST_DIRECT_EXCL", "0")
+    else:
+        monkeypatch.delenv("HRS_HOST_DIRECT_EXCL", raising=False)
+    return request.param
+
+
+@pytest.mark.usefixtures("direct_turns")
 def test_concurrent_calls_rows_sharing_pages(cuda):
     """Four threads, one codec each (one Encoder per mapper thread), whose
     rows are neighbours in one buffer (pages shared between the threads' rows):
-    no call registers a page another row reaches into, so the calls run
-    direct side by side; every result is bit-exact."""
+    no call registers a page another row reaches into, so overlapping direct
+    calls run side by side; every result is bit-exact."""
     n = K + P
     Ls = (128 << 10) + 16
     T, R = 4, 6
@@ -261,6 +274,7 @@ def test_concurrent_calls_rows_sharing_pages(cuda):
     assert set(paths) <= {"direct", "staged"} and "direct" in paths
 
 
+@pytest.mark.usefixtures("direct_turns")
 def test_concurrent_calls_sharing_input_rows(cuda):
     """Four threads encode the SAME input rows at once (a stripe read by
     several codecs): HIP would accept the same pages registered twice and
