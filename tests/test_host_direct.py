@@ -21,6 +21,7 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 K, P, L = 10, 4, 1 << 20
+DIRECT_FUZZ_SEED, DIRECT_FUZZ_CASES = 0xD1EC7, 40  # tools/fuzz_long.py runs other seeds
 
 
 @pytest.fixture(autouse=True)
@@ -368,10 +369,10 @@ def test_direct_fuzz(cuda):
     Non-codeword reads, bit-exact vs the oracle and zlib; at least half the
     calls must take the direct path (the rest are the staged fallbacks)."""
     import random
-    rnd = random.Random(0xD1EC7)
+    rnd = random.Random(DIRECT_FUZZ_SEED)
     fams = ["rs", "rs", "nrs", "xor", "src"]
     paths = []
-    for case in range(40):
+    for case in range(DIRECT_FUZZ_CASES):
         fam = fams[case % len(fams)]
         s = 0
         if fam == "rs":
