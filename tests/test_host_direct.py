@@ -21,7 +21,7 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 K, P, L = 10, 4, 1 << 20
-DIRECT_FUZZ_SEED, DIRECT_FUZZ_CASES = 0xD1EC7, 40  # tools/fuzz_long.py runs other seeds
+DIRECT_FUZZ_SEED, DIRECT_FUZZ_CASES = 0xD1EC7, 40  # tests/tools/fuzz_long.py runs other seeds
 
 
 @pytest.fixture(autouse=True)

@@ -3,7 +3,7 @@ in one process, calls interleaved: copy engine (pinned staging -> H2D ->
 kernel -> D2H, HRS_ZEROCOPY=0) vs zero copy (the kernel reads the staging and
 writes its outputs there across the host link), at one RS(10,4) 1 MiB-cell
 stripe per call — the shape Encoder.java:442 / Decoder.java:352 issue.
-Run: python tools/bench_host_ab.py [--calls 40] [--chunks 524288 ...]   (one JSON line)
+Run: python tests/tools/bench_host_ab.py [--calls 40] [--chunks 524288 ...]   (one JSON line)
 """
 import argparse
 import json
@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 from lambdafs_amd import HipReedSolomonCode  # noqa: E402

@@ -2,13 +2,13 @@
 tests/test_host_direct.py::test_direct_fuzz) with other seeds and more cases
 than the default `-m gpu` run affords: a bug hunt, not a test. Each seed is
 one call of the suite's own test function, so a failure names its case.
-Usage: python tools/fuzz_long.py [seeds] [cases] (one JSON line per seed)"""
+Usage: python tests/tools/fuzz_long.py [seeds] [cases] (one JSON line per seed)"""
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
