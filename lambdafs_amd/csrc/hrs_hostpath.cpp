@@ -283,17 +283,7 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     for (int i = 0; i < nin; ++i) {
       if (!din[i]) continue;
       in_m[i] = din[i] + c0;
-      if (W) {
-        in_ht[i] = h.pin_dev + W * j;
-        uint8_t* hr = h.pin + W * j;
-        uint8_t* tr = hr + ht_stride;
-        if (ncrc > 0) {  // the CRC reads the pads: zeros
-          std::memset(hr, 0, W - c0);
-          std::memset(tr, 0, W - tlen);
-        }
-        std::memcpy(hr + (W - c0), din[i], c0);
-        std::memcpy(tr + (W - tlen), din[i] + c1, tlen);
-      }
+      if (W) in_ht[i] = h.pin_dev + W * j;
       ++j;
     }
     for (int o = 0; o < nout; ++o, ++j) {
@@ -310,15 +300,30 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
       return apply_crc_impl(c, m, nout, nin, in.data(), stride, out.data(), stride, sl, nst, nullptr, cw, ss, raw);
     return run_apply(c, m, nout, nin, in.data(), stride, out.data(), stride, sl, nst, ss, static_kp);
   };
-  // the middle first, on slot 0's stream; the small head / tail launch
-  // follows on slot 1's, so it runs beside the middle instead of after it
+  // the middle is launched first, on slot 0's stream; the head / tail
+  // columns are copied into the staging while it runs and launched on slot
+  // 1's stream, beside it instead of after it
   uint32_t* raw_ht = c->direct_raw ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(c->direct_raw) + raw_mid)
                                    : nullptr;
   hrs_status rs = HRS_OK;
   {
     hrs::GridCap cap(zero_copy_blocks());
     rs = segment(in_m, out_m, 0, mid, 1, crc_dev + 2 * ncrc, s, c->direct_raw);
-    if (rs == HRS_OK && W) rs = segment(in_ht, out_ht, ht_stride, W, 2, crc_dev, s_ht, raw_ht);
+    if (rs == HRS_OK && W) {
+      int j = 0;
+      for (int i = 0; i < nin; ++i) {
+        if (!din[i]) continue;
+        uint8_t* hr = h.pin + W * j++;
+        uint8_t* tr = hr + ht_stride;
+        if (ncrc > 0) {  // the CRC reads the pads: zeros
+          std::memset(hr, 0, W - c0);
+          std::memset(tr, 0, W - tlen);
+        }
+        std::memcpy(hr + (W - c0), din[i], c0);
+        std::memcpy(tr + (W - tlen), din[i] + c1, tlen);
+      }
+      rs = segment(in_ht, out_ht, ht_stride, W, 2, crc_dev, s_ht, raw_ht);
+    }
   }
   // whatever the launches did, nothing may touch the pages once they are unregistered
   hipError_t e = hipStreamSynchronize(s);
