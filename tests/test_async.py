@@ -142,3 +142,29 @@ def test_wait_then_collect(cuda):
     assert all(np.array_equal(a, b) for a, b in zip(out, ref))
     with pytest.raises(HrsError):
         code.wait(t)  # collected: the ticket is gone
+
+
+def test_sync_calls_between_pending_rounds(cuda):
+    """Synchronous calls on the same handle while asynchronous rounds are in
+    flight (an Encoder that mixes encodeBulk and encodeBulkAsync): the
+    synchronous call runs over the caller's rows (its own streams and staging,
+    pages registered for the call) and leaves the pending rounds untouched;
+    every result vs the oracle."""
+    k, p, L = 10, 4, 1 << 20
+    code = HipReedSolomonCode(k, p, device=0, zero_inputs_after_encode=False)
+    rng = np.random.default_rng(77)
+    rounds = [[rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] for _ in range(3)]
+    keep = [[r.copy() for r in rnd] for rnd in rounds]
+    tickets = [code.encodeBulkAsync(r) for r in rounds]
+    sync_data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    sync_par = [np.zeros(L, np.uint8) for _ in range(p)]
+    crcs = code.encodeBulkCrc(sync_data, sync_par)
+    ref = C.encode_bulk(k, p, sync_data)
+    assert all(np.array_equal(a, b) for a, b in zip(sync_par, ref))
+    assert crcs == [zlib.crc32(b.tobytes()) for b in sync_data + list(ref)]
+    for t, kept in reversed(list(zip(tickets, keep))):
+        out = [np.full(L, 0xEE, np.uint8) for _ in range(p)]
+        code.collect(t, out)
+        want = C.encode_bulk(k, p, kept)
+        assert all(np.array_equal(a, b) for a, b in zip(out, want))
+    assert code.pending() == 0
