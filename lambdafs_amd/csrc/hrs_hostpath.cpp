@@ -186,9 +186,7 @@ void RegisteredPages::release() {
   ok_ = false;
 }
 
-// Runs the call over the caller's rows; false (nothing done, nothing left
-// registered) when the call must take the staged path. *st: its status.
-// One direct call at a time per process: a call that finds another one in
+// One direct call at a time per device: a call that finds another one in
 // flight takes the staged path. One direct caller already fills the host
 // link; beside it, the staged callers' host copies overlap its link time,
 // where overlapping direct calls only split the link (and churn
@@ -196,17 +194,25 @@ void RegisteredPages::release() {
 // way, 31.9-34.9 with direct calls overlapping, 35.3-38.1 all staged
 // (profiles/r05/NOTES.md). HRS_HOST_DIRECT_EXCL=0 lets them overlap (A/B
 // runs; read per call).
-std::atomic<int> g_direct_inflight{0};
+// The turn is per device: each GPU has its own host link, so codecs on
+// different devices (a device set, one Encoder per GPU) go direct side by side.
+constexpr int kTurnSlots = 64;  // devices beyond share the last slot
+std::atomic<int> g_direct_inflight[kTurnSlots];
 struct DirectTurn {
   bool ok = true;
-  DirectTurn() {
+  std::atomic<int>& n;
+  explicit DirectTurn(int device) : n(g_direct_inflight[std::min(std::max(device, 0), kTurnSlots - 1)]) {
     const char* e = getenv("HRS_HOST_DIRECT_EXCL");
-    const int before = g_direct_inflight.fetch_add(1);
+    const int before = n.fetch_add(1);
     if (!(e && e[0] == '0') && before > 0) ok = false;
   }
-  ~DirectTurn() { g_direct_inflight.fetch_sub(1); }
+  ~DirectTurn() { n.fetch_sub(1); }
+  DirectTurn(const DirectTurn&) = delete;
+  DirectTurn& operator=(const DirectTurn&) = delete;
 };
 
+// Runs the call over the caller's rows; false (nothing done, nothing left
+// registered) when the call must take the staged path. *st: its status.
 bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
                        uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc, int nlive,
                        hrs_status* st) {
@@ -266,7 +272,7 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
     *st = s0;
     return true;
   }
-  DirectTurn turn;
+  DirectTurn turn(c->device);
   if (!turn.ok) return false;
   RegisteredPages reg(std::move(rg));  // merged: a row passed twice, or rows back to back, register once
   if (!reg.ok()) return false;
