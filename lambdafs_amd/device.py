@@ -38,6 +38,23 @@ def _rows(views):
     return ptrs, stride, L, S
 
 
+def _stripe_rows(t, locs):
+    """Rows `locs` (None = not passed) of a [S, m, L] uint8 device tensor ->
+    (pointer array, stride bytes, L, S), the same as _rows over the views
+    t[:, loc, :] but computed from t's own pointer and strides: building m
+    tensor views costs ~3 us each in Python, more than a small launch."""
+    torch = _lib.torch
+    if t.dtype != torch.uint8 or t.dim() != 3 or t.stride(2) != 1 or not t.is_cuda:
+        raise ValueError("stripes must be a [S, m, L] uint8 device tensor with unit byte stride")
+    S, m, L = t.shape
+    base, s_stripe, s_row = t.data_ptr(), t.stride(0), t.stride(1)
+    for loc in locs:
+        if loc is not None and not 0 <= loc < m:
+            raise ValueError(f"row {loc} outside [0, {m})")
+    ptrs = ptr_array([None if loc is None else base + loc * s_row for loc in locs])
+    return ptrs, (s_stripe if S > 1 else L), L, S
+
+
 def _stream(t):
     return _lib.torch.cuda.current_stream(t.device).cuda_stream
 
@@ -47,8 +64,8 @@ def encode_stripes(code, stripes):
     k, p = code.stripeSize(), code.paritySize()
     if stripes.dim() != 3 or stripes.shape[1] != k + p:
         raise ValueError(f"stripes must be [S, {k + p}, L]")
-    ins, s_in, L, S = _rows([stripes[:, p + c, :] for c in range(k)])
-    outs, s_out, _, _ = _rows([stripes[:, r, :] for r in range(p)])
+    ins, s_in, L, S = _stripe_rows(stripes, range(p, p + k))
+    outs, s_out, _, _ = _stripe_rows(stripes, range(p))
     code._check(_lib.lib().hrs_encode_dev(code._handle(), ins, s_in, outs, s_out, L, S, _stream(stripes)))
 
 
@@ -63,8 +80,8 @@ def encode_stripes_crc(code, stripes, crc_in=None):
     k, p = code.stripeSize(), code.paritySize()
     if stripes.dim() != 3 or stripes.shape[1] != k + p:
         raise ValueError(f"stripes must be [S, {k + p}, L]")
-    ins, s_in, L, S = _rows([stripes[:, p + c, :] for c in range(k)])
-    outs, s_out, _, _ = _rows([stripes[:, r, :] for r in range(p)])
+    ins, s_in, L, S = _stripe_rows(stripes, range(p, p + k))
+    outs, s_out, _, _ = _stripe_rows(stripes, range(p))
     crc = torch.empty((S, k + p), dtype=torch.int32, device=stripes.device)
     cin = None
     if crc_in is not None:
@@ -92,8 +109,8 @@ def decode_stripes(code, stripes, erased, not_to_read, out):
     if stripes.dim() != 3 or stripes.shape[1] != n:
         raise ValueError(f"stripes must be [S, {n}, L]")
     ntr = set(not_to_read)
-    rows, s_in, L, S = _rows([None if loc in ntr else stripes[:, loc, :] for loc in range(n)])
-    outs, s_out, L2, S2 = _rows([out[:, i, :] for i in range(len(erased))])
+    rows, s_in, L, S = _stripe_rows(stripes, [None if loc in ntr else loc for loc in range(n)])
+    outs, s_out, L2, S2 = _stripe_rows(out, range(len(erased)))
     if (L, S) != (L2, S2):
         raise ValueError("out must be [S, e, L]")
     code._check(_lib.lib().hrs_decode_dev(
@@ -112,8 +129,8 @@ def decode_stripes_crc(code, stripes, erased, not_to_read, out, crc_in=None):
     if stripes.dim() != 3 or stripes.shape[1] != n:
         raise ValueError(f"stripes must be [S, {n}, L]")
     ntr = set(not_to_read)
-    rows, s_in, L, S = _rows([None if loc in ntr else stripes[:, loc, :] for loc in range(n)])
-    outs, s_out, L2, S2 = _rows([out[:, i, :] for i in range(len(erased))])
+    rows, s_in, L, S = _stripe_rows(stripes, [None if loc in ntr else loc for loc in range(n)])
+    outs, s_out, L2, S2 = _stripe_rows(out, range(len(erased)))
     if (L, S) != (L2, S2):
         raise ValueError("out must be [S, e, L]")
     crc = torch.empty((S, len(erased)), dtype=torch.int32, device=stripes.device)
