@@ -22,7 +22,7 @@ JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
             tests/cpp/copy_pool_test tests/cpp/page_claims_test
 
-TOOLS    := tools/host_call_rate tools/register_zc_probe
+TOOLS    := tools/host_call_rate tools/register_zc_probe tools/register_par_probe
 
 all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
 
@@ -33,6 +33,10 @@ tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
 # Staged vs page-registered synchronous calls (profiles/r05/NOTES.md).
 tools/register_zc_probe: tools/register_zc_probe.cpp include/hrs.h $(LIB)
 	$(HIPCC) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
+
+# Serial vs multi-threaded registration of a call's rows (profiles/r05/NOTES.md).
+tools/register_par_probe: tools/register_par_probe.cpp
+	$(HIPCC) -O2 -std=c++17 -Wall -pthread -o $@ $<
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build
