@@ -124,11 +124,23 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
 // at least 32 KiB, a checksummed call's middle kernel is one-pass (a
 // two-pass CRC would read the cells across the link twice), no other call of
 // this process holds any of its pages (PageClaims) and every range registers
-// (pages the caller registered fail it). Otherwise the call takes the staged path, with the same results.
-// HRS_HOST_DIRECT=0 turns it off (A/B runs; read per call).
+// (pages the caller registered fail it). Otherwise the call takes the staged
+// path, with the same results.
+// OFF BY DEFAULT (HRS_HOST_DIRECT=1 turns it on; read per call). A
+// registration maps the caller's pageable pages without pinning them (the
+// driver's userptr objects follow the pages through MMU notifiers), and in
+// long runs of the seeded fuzz suites (tests/tools/fuzz_long.py) a direct call
+// now and then lost the GPU's writes to one page of an output row from one
+// window on: the pattern of a page the kernel moved (THP collapse, compaction)
+// or a stale GPU translation while the kernel ran (profiles/r05/NOTES.md,
+// "Direct path: intermittent lost writes"). Pinned staging
+// (hipHostMalloc'd, never moved) has no such window, so it is the default;
+// the direct path stays for callers whose memory cannot move during a call
+// (hugetlbfs-backed, or a host configured without THP collapse and
+// compaction of unevictable pages).
 bool host_direct_on() {
   const char* e = getenv("HRS_HOST_DIRECT");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 // Shortest row the direct path takes: HRS_HOST_DIRECT_MIN for plain calls

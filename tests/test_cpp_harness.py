@@ -13,10 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "tests", "cpp", "codec_harness")
 
 
-def run(*args, timeout=600):
+def run(*args, timeout=600, env=None):
     if not os.path.exists(HARNESS):
         subprocess.check_call(["make", "-C", ROOT, "tests/cpp/codec_harness"])
-    out = subprocess.run([HARNESS, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    out = subprocess.run([HARNESS, *map(str, args)], capture_output=True, text=True, timeout=timeout,
+                         env=None if env is None else dict(os.environ, **env))
     line = out.stdout.strip().splitlines()[-1]
     return out.returncode, json.loads(line)
 
@@ -122,14 +123,18 @@ def test_harness_decoder_restart_mid_block(cuda, args):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("direct", ["0", "1"])
 @pytest.mark.parametrize("threads", [2, 4])
-def test_harness_concurrent_handles(cuda, threads):
+def test_harness_concurrent_handles(cuda, threads, direct):
     """One codec per thread (Encoder.java:80, Decoder.java:90,
     MapReduceBlockRepairManager.java:426): threads interleave encodeBulk and
     decodeBulk (1-4 lost locations, changing every round) of RS(10,4) 1 MiB
     cells on their own handles; every round bit-exact vs the oracle's parity
-    and the original cells."""
-    rc, res = run(f"--threads={threads}", "--rounds=12", 10, 4, 1 << 20, 1 << 20, 1, 31)
+    and the original cells. Staged (the default) and with the opt-in direct
+    path (HRS_HOST_DIRECT=1, overlapping calls allowed so the page claims
+    see shared rows)."""
+    env = {"HRS_HOST_DIRECT": direct, "HRS_HOST_DIRECT_EXCL": "0"}
+    rc, res = run(f"--threads={threads}", "--rounds=12", 10, 4, 1 << 20, 1 << 20, 1, 31, env=env)
     assert rc == 0 and res["ok"], res
 
 

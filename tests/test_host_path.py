@@ -14,15 +14,15 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True, params=["direct", "zero_copy", "copy_engine"])
 def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
-    bytes: straight over the caller's rows (the default where they qualify:
-    their pages registered for the call, the zero-copy kernel reads and writes
-    them in place), the staged zero-copy path (HRS_HOST_DIRECT=0: rows copied
-    into pinned staging, the kernel works on the staging) and the copy engine
-    (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
+    bytes: the staged zero-copy path (the default: rows copied into pinned
+    staging, the kernel works on the staging across the link), straight over
+    the caller's rows (opt-in, HRS_HOST_DIRECT=1: their pages registered for
+    the call, the zero-copy kernel reads and writes them in place) and the
+    copy engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H)."""
     monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
-    if request.param == "zero_copy":
-        monkeypatch.setenv("HRS_HOST_DIRECT", "0")
+    if request.param == "direct":
+        monkeypatch.setenv("HRS_HOST_DIRECT", "1")
     elif request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
     return request.param

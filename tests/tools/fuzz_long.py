@@ -21,6 +21,16 @@ import test_host_direct as D  # noqa: E402
 def main():
     seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     cases = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+    if "--no-thp" in sys.argv:  # numpy stops madvise(MADV_HUGEPAGE) on its large arrays
+        import numpy._core.multiarray as ma
+        ma._set_madvise_hugepage(False)
+    if "--local-mempolicy" in sys.argv:
+        # MPOL_LOCAL for the whole process: with an explicit policy (no
+        # MPOL_F_NUMA_BALANCING) the kernel's NUMA balancing leaves its pages alone
+        import ctypes
+        libc = ctypes.CDLL(None, use_errno=True)
+        if libc.syscall(238, 4, None, 0) != 0:  # SYS_set_mempolicy, MPOL_LOCAL
+            raise SystemExit(f"set_mempolicy failed: errno {ctypes.get_errno()}")
     if not torch.cuda.is_available():
         raise SystemExit("no HIP device")
     F.CASES = cases
