@@ -241,7 +241,7 @@ def host_calls(local, calls=100):
         return (time.perf_counter() - t0) * 1e3 / calls
 
     res = {"what": "synchronous host-buffer calls through the C ABI (the JNI shim's calls), RS(10,4), one stripe of "
-                   "1 MiB pageable rows per call", "calls": calls}
+                   "1 MiB pageable rows per call (pinned_rows: the same on caller-pinned rows)", "calls": calls}
     res["encodeBulk_ms"] = per_call(lambda: lib.hrs_encode(h, ins, outs, L))
     res["decodeBulk_ms"] = per_call(lambda: lib.hrs_decode(h, reads, lostp, e_a, 1, t_a, k, n_a, len(ntr), L))
     ok = bool(np.array_equal(lost, rows[p]))
@@ -252,6 +252,17 @@ def host_calls(local, calls=100):
     for key in ("encodeBulk", "decodeBulk", "encodeBulkCrc", "decodeBulkCrc"):
         res[key + "_ms"] = round(res[key + "_ms"], 4)
         res[key + "_GiBps_user"] = round(k * L / GiB / (res[key + "_ms"] * 1e-3), 2)
+    # the same calls on rows the caller holds in pinned memory (hipHostMalloc,
+    # via torch): the kernel runs over them in place, no staging ("pinned")
+    pin = torch.empty((n, L), dtype=torch.uint8, pin_memory=True).numpy()
+    pin[:] = np.stack(rows)
+    pins = ptr_array([pin[i].ctypes.data for i in range(p, n)])
+    pouts = ptr_array([pin[i].ctypes.data for i in range(p)])
+    res["pinned_rows"] = {"encodeBulk_ms": round(per_call(lambda: lib.hrs_encode(h, pins, pouts, L)), 4),
+                          "encodeBulkCrc_ms": round(per_call(lambda: lib.hrs_encode_crc(h, pins, pouts, L, None, crc)),
+                                                    4),
+                          "path": code.lastHostPath()}
+    ok &= all(np.array_equal(pin[r], rows[r]) for r in range(p))
     res["bit_exact"] = ok
     if not ok:
         raise RuntimeError("host-buffer decode did not reproduce the lost row")

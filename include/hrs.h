@@ -110,12 +110,12 @@ const char* hrs_last_error(const hrs_codec* codec);
 const char* hrs_last_kernel(const hrs_codec* codec);
 /* How the handle's latest synchronous host-buffer call (hrs_encode, hrs_decode,
  * hrs_decode3, hrs_*_crc) or host batch (hrs_*_batch_host) moved its bytes:
- * "direct" (the zero-copy kernel read and wrote the caller's pageable memory
- * in place, its pages registered for the call), "pinned" (a batch in the
- * caller's pinned memory, zero copy), "staged" (copied through pinned
- * staging, the zero-copy kernel on the staging), "copy_engine" (staging, H2D,
- * kernel, D2H), or "" before any such call. Diagnostic, like
- * hrs_last_kernel. */
+ * "pinned" (rows or batch in the caller's pinned memory: the zero-copy kernel
+ * in place), "staged" (pageable memory copied through pinned staging, the
+ * zero-copy kernel on the staging; the default), "direct" (opt-in,
+ * HRS_HOST_DIRECT=1: pageable memory registered for the call, the kernel in
+ * place), "copy_engine" (staging, H2D, kernel, D2H), or "" before any such
+ * call. Diagnostic, like hrs_last_kernel. */
 const char* hrs_last_host_path(const hrs_codec* codec);
 const char* hrs_version(void);
 

@@ -378,6 +378,64 @@ bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
   return true;
 }
 
+// Rows the caller already holds in pinned memory (hipHostMalloc'd, or
+// registered by the caller) are visible to the GPU at their own addresses and
+// never move: the zero-copy kernel runs over them in place, one launch, no
+// staging copies and no registrations ("pinned"). Taken when zero copy is on,
+// every live input and output row is pinned and 16-byte aligned, and a
+// checksummed call's kernel is one-pass (a two-pass CRC would read the cells
+// across the link twice); otherwise false and nothing done.
+bool host_apply_pinned(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
+                       uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc,
+                       hrs_status* st) {
+  if (!zero_copy_on()) return false;
+  int nlive = 0;
+  for (int i = 0; i < nin; ++i) {
+    if (!din[i]) continue;
+    uint8_t* d = nullptr;
+    if (!aligned16(din[i]) || !host_device_ptr(din[i], &d) || d != din[i]) return false;
+    ++nlive;
+  }
+  for (int o = 0; o < nout; ++o) {
+    uint8_t* d = nullptr;
+    if (!aligned16(out_rows[o]) || !host_device_ptr(out_rows[o], &d) || d != out_rows[o]) return false;
+  }
+  if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, len, 1)) return false;
+  if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, len)) return false;
+  // the chunk CRC words in slot 0's pinned staging, the raw window CRCs in its device buffer
+  const size_t words = static_cast<size_t>(std::max(ncrc, 1)) * sizeof(uint32_t);
+  const size_t raw_off = (words + 255) & ~static_cast<size_t>(255);
+  hrs_status s0 = host_slot(c, 0, ncrc > 0 ? raw_off + crc_raw_bytes_for(len, 1, ncrc) : words);
+  if (s0 == HRS_OK && !c->host[0].pin_dev) return false;
+  if (s0 != HRS_OK) {
+    *st = s0;
+    return true;
+  }
+  hrs_codec::HostSlot& h = c->host[0];
+  c->last_host_path = "pinned";
+  uint32_t* cw = reinterpret_cast<uint32_t*>(h.pin_dev);
+  uint32_t* raw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
+  hrs_status rs = HRS_OK;
+  {
+    hrs::GridCap cap(zero_copy_blocks());
+    if (crc.mode == kCrcEncode)
+      rs = encode_crc_impl(c, din, 0, out_rows, 0, len, 1, nullptr, cw, h.stream, raw);
+    else if (crc.mode == kCrcOutputs)
+      rs = apply_crc_impl(c, m, nout, nin, din, 0, out_rows, 0, len, 1, nullptr, cw, h.stream, raw);
+    else
+      rs = run_apply(c, m, nout, nin, din, 0, out_rows, 0, len, 1, h.stream, static_kp);
+  }
+  const hipError_t e = hipStreamSynchronize(h.stream);
+  if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
+  if (rs == HRS_OK && ncrc > 0) {  // CRC32.update chaining from the running values
+    const uint32_t* part = reinterpret_cast<const uint32_t*>(h.pin);
+    const hrs::crc::Mat& z = crc_zmat(c, len);
+    for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[r];
+  }
+  *st = rs;
+  return true;
+}
+
 hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                            uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc) {
   const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
@@ -402,6 +460,7 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     std::vector<const uint8_t*> live_rows(nin);
     for (int i = 0; i < nin; ++i) live_rows[i] = slot_of[i] >= 0 ? in_rows[i] : nullptr;
     hrs_status st = HRS_OK;
+    if (host_apply_pinned(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, &st)) return st;
     if (host_apply_direct(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, nlive, &st)) return st;
   }
   const size_t chunk = std::min(len, host_chunk_bytes());

@@ -94,10 +94,11 @@ def test_fallbacks(cuda):
     buf = rng.integers(0, 256, (K + P) * (L + 8) + 64, dtype=np.uint8)
     rows = _rows_in(buf, K + P, L, 8, 8)
     _encode_check(code, rows[:K], rows[K:], "staged")
-    # pinned rows (hipHostMalloc'd by torch): registration fails, staged path
+    # pinned rows (hipHostMalloc'd by torch): nothing to register, the kernel
+    # runs over them in place (the "pinned" path comes first)
     pin = torch.empty((K + P, L), dtype=torch.uint8, pin_memory=True).numpy()
     pin[:K] = rng.integers(0, 256, (K, L), dtype=np.uint8)
-    _encode_check(code, list(pin[:K]), list(pin[K:]), "staged")
+    _encode_check(code, list(pin[:K]), list(pin[K:]), "pinned")
     # short rows: below HRS_HOST_DIRECT_MIN the copies cost less than registering
     small = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(K)]
     out = [np.zeros(4096, np.uint8) for _ in range(P)]

@@ -61,3 +61,39 @@ def test_host_nrs_and_xor_multi_chunk(cuda):
     xp = [np.zeros(L, np.uint8)]
     xor.encodeBulk(data, xp)
     assert (xp[0] == C.xor_encode_bulk(10, data)).all()
+
+
+@pytest.mark.parametrize("L", [1 << 20, (1 << 20) + 48, 4096 + 16])
+def test_host_calls_on_pinned_rows(cuda, transfer_mode, L):
+    """Rows the caller holds in pinned memory (torch pin_memory, i.e.
+    hipHostMalloc) go straight to the zero-copy kernel in place ("pinned"; the
+    copy engine mode stages them): encodeBulk, encodeBulkCrc and the 5-arg
+    decodeBulkCrc vs the oracle and zlib."""
+    import zlib
+    torch = cuda
+    k, p = 10, 4
+    n = k + p
+    code = HipReedSolomonCode(k, p, zero_inputs_after_encode=False)
+    buf = torch.empty((n + 2, L), dtype=torch.uint8, pin_memory=True).numpy()
+    rng = np.random.default_rng(L)
+    buf[p:n] = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    data, par = list(buf[p:n]), list(buf[:p])
+    ref = C.encode_bulk(k, p, [d.copy() for d in data])
+    want_path = "copy_engine" if transfer_mode == "copy_engine" else "pinned"
+    code.encodeBulk(data, par)
+    assert code.lastHostPath() == want_path
+    assert all(np.array_equal(par[o], ref[o]) for o in range(p))
+    buf[:p] = 0
+    crcs = code.encodeBulkCrc(data, par, [3] * n)
+    assert all(np.array_equal(par[o], ref[o]) for o in range(p))
+    assert crcs == [zlib.crc32(r.tobytes(), 3) for r in data + list(ref)]
+    stripe = list(buf[:n])
+    erased = [p + 2]
+    tr = sorted(C.locations_to_read(k, p, erased))
+    ntr = [x for x in range(n) if x not in tr]
+    out = [buf[n]]
+    dcrc = code.decodeBulkCrc([stripe[x] if x in tr else None for x in range(n)], out, erased, tr, ntr, [9])
+    assert np.array_equal(out[0], data[2])
+    assert dcrc == [zlib.crc32(data[2].tobytes(), 9)]
+    if L % 2048 == 0:  # a ragged checksummed repair has no one-pass kernel: it is staged
+        assert code.lastHostPath() == want_path
