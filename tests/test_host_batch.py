@@ -21,24 +21,19 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "direct", "copy_engine", "duplex"])
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "duplex"])
 def transfer_mode(request, monkeypatch):
     """Every test runs every way the host batches can move bytes: zero copy
     (the default: kernels read and write pinned host memory across the link;
-    pageable batches go through pinned staging slots), pageable batches with
-    their pages registered for the call (opt-in, HRS_HOST_DIRECT=1, the
-    "direct" path: the stripes inside whole pages zero copy, the few at either
-    end staged), the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D,
+    pageable batches go through pinned staging slots), the copy engine (HRS_ZEROCOPY=0: pinned staging, H2D,
     kernel, D2H on each slot's stream), and the copy engine with the
     directions split over the shared copy-in / copy-out streams
     (HRS_HBATCH_DUPLEX=1: in_done / comp_done / done events chain the three
     streams per slot)."""
     monkeypatch.delenv("HRS_HBATCH_DUPLEX", raising=False)
     monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
-    if request.param in ("zero_copy", "direct"):
+    if request.param == "zero_copy":
         monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
-        if request.param == "direct":
-            monkeypatch.setenv("HRS_HOST_DIRECT", "1")
     else:
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
         if request.param == "duplex":
@@ -246,7 +241,7 @@ def test_pageable_batches_path_and_parity(cuda, transfer_mode, offset):
     oraw = np.empty(S * 2 * L + offset + 8192, np.uint8)
     obase = (-oraw.ctypes.data) % 4096 + offset
     out = oraw[obase:obase + S * 2 * L].reshape(S, 2, L)
-    want = {"zero_copy": "staged", "direct": "direct", "copy_engine": "copy_engine", "duplex": "copy_engine"}
+    want = {"zero_copy": "staged", "copy_engine": "copy_engine", "duplex": "copy_engine"}
     device.encode_batch_host(code, st)
     assert code.lastHostPath() == want[transfer_mode]
     for s in range(S):
@@ -262,15 +257,15 @@ def test_pageable_batches_path_and_parity(cuda, transfer_mode, offset):
     pin[:] = st
     pout = _alloc(torch, (S, 2, L), True)
     device.decode_batch_host(code, pin, er, pout)
-    assert code.lastHostPath() == ("pinned" if transfer_mode in ("zero_copy", "direct") else "copy_engine")
+    assert code.lastHostPath() == ("pinned" if transfer_mode == "zero_copy" else "copy_engine")
     assert np.array_equal(pout, out)
 
 
-def test_pageable_multi_batch_direct(cuda, transfer_mode):
+def test_pageable_multi_batch(cuda, transfer_mode):
     """hrs_decode_batch_host_multi over the device set {0, 0} on pageable
-    memory: with the direct path on, each member registers the whole pages of its own stripe range
-    (the page the two ranges share belongs to neither and its stripes are
-    staged); every repaired cell and every parity row checked."""
+    memory starting 48 bytes past a page boundary: every repaired cell and
+    every parity row checked (test_host_direct.py runs the same with the
+    opt-in direct path)."""
     k, p, S, L = 12, 4, 16, 64 << 10
     n = k + p
     codes = [HipReedSolomonCode(k, p, device=0) for _ in range(2)]
@@ -289,5 +284,3 @@ def test_pageable_multi_batch_direct(cuda, transfer_mode):
     for s in range(S):
         lost = [int(x) for x in er[s] if x >= 0]
         assert np.array_equal(out[s, :len(lost)], st[s, lost]), (s, lost)
-    if transfer_mode == "direct":
-        assert [c.lastHostPath() for c in codes] == ["direct", "direct"]
