@@ -166,7 +166,11 @@ hrs_status hrs_encode_matrix(const hrs_codec* codec, uint8_t* g);
  *   syndromes, erased locations absent from not_to_read decode to 0.
  * zero_not_to_read = 0: decodeBulk 3-arg semantics (ReedSolomonCode.java:168-185):
  *   not_to_read is the erased list itself, nothing is zeroed.
- * Locations must be distinct and in [0, n). */
+ * RS: D is the reference decode run on unit vectors, so it reproduces the
+ * Java on every list the Java accepts: repeated locations (a division by zero
+ * in solveVandermondeSystem yields 0, GaloisField.java:107-118) and, in the
+ * 5-arg form, erased locations of any value (only compared with not_to_read).
+ * not_to_read locations (and 3-arg erased ones) must be in [0, n). */
 hrs_status hrs_decode_matrix(const hrs_codec* codec, const int* erased, int num_erased,
                              const int* not_to_read, int num_not_to_read, int zero_not_to_read,
                              uint8_t* d);

@@ -46,9 +46,22 @@ hrs_status hip_fail(hrs_codec* c, hipError_t e, const char* what) {
   return fail(c, HRS_EDEVICE, "%s: %s", what, hipGetErrorString(e));
 }
 
-bool sorted_unique_ok(const int* v, int nv, int n) {
+static bool in_range(const int* v, int nv, int n) {
   for (int i = 0; i < nv; ++i)
     if (v[i] < 0 || v[i] >= n) return false;
+  return true;
+}
+
+// Location lists of a 5-arg decode, as the reference indexes them: not-to-read
+// locations always (primitivePower / data), erased ones except in
+// ReedSolomonCode (it only compares them, ReedSolomonCode.java:158-165), and
+// locationsToRead only in SimpleRegeneratingCode (RS, nrs and XOR ignore it).
+// Repeats are allowed: the Java accepts them (hrs_matrix.cpp rs_decode_rows).
+bool decode_locations_ok(const hrs_codec* c, const int* erased, int ne, const int* to_read, int nr, const int* ntr,
+                         int nn) {
+  if (!in_range(ntr, nn, c->n)) return false;
+  if (c->kind != HRS_CODE_RS && !in_range(erased, ne, c->n)) return false;
+  if (c->kind == HRS_CODE_SRC && to_read && !in_range(to_read, nr, c->n)) return false;
   return true;
 }
 

@@ -199,11 +199,12 @@ class RegisteredPages {
 // them. SRC's G (XOR groups over RS(k, r)) and XOR's all-ones row may not.
 inline bool static_encode_family(const hrs_codec* c) { return c->kind == HRS_CODE_RS || c->kind == HRS_CODE_NRS; }
 
-bool sorted_unique_ok(const int* v, int nv, int n);
+bool decode_locations_ok(const hrs_codec* c, const int* erased, int ne, const int* to_read, int nr, const int* ntr,
+                         int nn);
 
 // ---- matrices (hrs_matrix.cpp)
 bool gf_invert(std::vector<uint8_t>& a, int m);
-bool rs_decode_rows(int n, const int* erased, int ne, const int* ntr, int nn, int zero_ntr, std::vector<uint8_t>& d);
+void rs_decode_rows(int n, const int* erased, int ne, const int* ntr, int nn, int zero_ntr, std::vector<uint8_t>& d);
 hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn, int zero_ntr,
                                std::vector<uint8_t>& d);
 hrs_status build_nrs_decode_matrix(hrs_codec* c, int ne, const int* ntr, int nn, std::vector<uint8_t>& d);

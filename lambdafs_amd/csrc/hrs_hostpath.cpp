@@ -750,8 +750,7 @@ hrs_status hrs_decode_crc(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t
   if (!read_bufs || (ne > 0 && (!write_bufs || !erased || !crc_out)) || ne < 0 || nn < 0 || nr < 0 ||
       (nn > 0 && !ntr))
     return fail(c, HRS_EINVAL, "bad decode arguments");
-  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) ||
-      (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+  if (!decode_locations_ok(c, erased, ne, to_read, nr, ntr, nn))
     return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
   if (ne == 0) return HRS_OK;
   std::vector<uint8_t> tmp;
@@ -771,7 +770,7 @@ hrs_status hrs_decode(hrs_codec* c, const uint8_t* const* read_bufs, uint8_t* co
   (void)to_read;
   if (!read_bufs || (ne > 0 && (!write_bufs || !erased)) || ne < 0 || nn < 0 || nr < 0 || (nn > 0 && !ntr))
     return fail(c, HRS_EINVAL, "bad decode arguments");
-  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) || (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+  if (!decode_locations_ok(c, erased, ne, to_read, nr, ntr, nn))
     return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
   if (ne == 0 && c->kind == HRS_CODE_RS) return HRS_OK;
   std::vector<uint8_t> tmp;
@@ -815,8 +814,7 @@ hrs_status hrs_decode_submit(hrs_codec* c, const uint8_t* const* read_bufs, cons
   if (!c) return HRS_EINVAL;
   if (!read_bufs || ne < 0 || nn < 0 || nr < 0 || (ne > 0 && !erased) || (nn > 0 && !ntr))
     return fail(c, HRS_EINVAL, "bad decode arguments");
-  if (!sorted_unique_ok(erased, ne, c->n) || !sorted_unique_ok(ntr, nn, c->n) ||
-      (to_read && !sorted_unique_ok(to_read, nr, c->n)))
+  if (!decode_locations_ok(c, erased, ne, to_read, nr, ntr, nn))
     return fail(c, HRS_EINVAL, "location out of range [0,%d)", c->n);
   std::vector<uint8_t> tmp;
   const uint8_t* d = nullptr;

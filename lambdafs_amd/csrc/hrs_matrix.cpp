@@ -57,51 +57,89 @@ bool gf_invert(std::vector<uint8_t>& a, int m) {
   return true;
 }
 
-// Decode rows in closed form over an RS stripe of n locations (see hrs.h).
-// With x_j = alpha^ntr[j] and syndromes S_i = sum_l A[i][l] d_l,
-// A[i][l] = alpha^(i*l) (0 where zeroed), the reference solves V z = S with
-// V[i][j] = x_j^i (GaloisField.java:232-246; ReedSolomonCode.java:127-142),
-// so z = V^-1 A d. Locations are validated by the caller.
-bool rs_decode_rows(int n, const int* erased, int ne, const int* ntr, int nn, int zero_ntr, std::vector<uint8_t>& d) {
-  d.assign(static_cast<size_t>(ne) * n, 0);
-  if (ne == 0 || nn == 0) return true;
-  std::vector<char> in_ntr(n, 0);
-  for (int j = 0; j < nn; ++j) in_ntr[ntr[j]] = 1;
-  const int m = nn;
-  std::vector<uint8_t> v(static_cast<size_t>(m) * m);
-  for (int i = 0; i < m; ++i)
-    for (int j = 0; j < m; ++j) v[i * m + j] = gf::alpha_pow(static_cast<long>(ntr[j]) * i);
-  if (!gf_invert(v, m)) return false;
-  for (int t = 0; t < ne; ++t) {
-    int j = -1;
-    for (int q = 0; q < nn; ++q)
-      if (ntr[q] == erased[t]) {
-        j = q;
-        break;
-      }
-    if (j < 0) continue;  // not in not_to_read: stays 0 (ReedSolomonCode.java:158-165)
+// GaloisField.divide through the reference's table (GaloisField.java:107-118):
+// divTable[a][0] is never written, so a division by zero yields 0. It happens
+// when a location list repeats an entry (x_j ^ x_{j-i-1} == 0 in the solve).
+constexpr uint8_t java_div(uint8_t a, uint8_t b) { return b == 0 ? 0 : gf::div(a, b); }
+
+// ReedSolomonCode.decode 3-arg (ReedSolomonCode.java:127-142) on one column
+// of symbols: zero the locations (zero_locs; the bulk 3-arg decodeBulk,
+// :168-185, substitutes the rows as they are), syndromes S_i = data(alpha^i)
+// (GaloisField.substitute, :375-383), then GaloisField.solveVandermondeSystem
+// (:232-246) in place. values[nl].
+void rs_decode_column(int n, uint8_t* data, const int* loc, int nl, bool zero_locs, uint8_t* values) {
+  if (nl == 0) return;
+  if (zero_locs)
+    for (int i = 0; i < nl; ++i) data[loc[i]] = 0;
+  std::vector<uint8_t> x(nl);
+  for (int i = 0; i < nl; ++i) {
+    x[i] = gf::alpha_pow(loc[i]);
+    const uint8_t a = gf::alpha_pow(i);
+    uint8_t r = 0, y = 1;
     for (int l = 0; l < n; ++l) {
-      if (zero_ntr && in_ntr[l]) continue;
-      uint8_t acc = 0;
-      for (int i = 0; i < m; ++i) acc ^= gf::mul(v[j * m + i], gf::alpha_pow(static_cast<long>(i) * l));
-      d[static_cast<size_t>(t) * n + l] = acc;
+      r ^= gf::mul(data[l], y);
+      y = gf::mul(a, y);
     }
+    values[i] = r;
   }
-  return true;
+  for (int i = 0; i < nl - 1; ++i)
+    for (int j = nl - 1; j > i; --j) values[j] ^= gf::mul(x[i], values[j - 1]);
+  for (int i = nl - 1; i >= 0; --i) {
+    for (int j = i + 1; j < nl; ++j) values[j] = java_div(values[j], x[j] ^ x[j - i - 1]);
+    for (int j = i; j < nl - 1; ++j) values[j] ^= values[j + 1];
+  }
 }
 
+// The decode rows over an RS stripe of n locations (see hrs.h), built as
+// SURVEY §0.3 prescribes: the reference decode runs on every unit vector e_l
+// and its outputs form column l. The decode is GF(2^8)-linear in the data
+// (every division is by a value of the locations alone), so D * stripe
+// reproduces the Java byte for byte on every input it accepts, repeated
+// locations and erased locations outside not_to_read included.
+//  zero_ntr = 1, decodeBulk 5-arg (:144-166, :191-211): decode over ntr with
+//    ntr zeroed; output t copies the FIRST ntr entry equal to erased[t], and
+//    stays 0 when there is none (an erased value of any range).
+//  zero_ntr = 0, decodeBulk 3-arg (ntr is the erased list): nothing zeroed,
+//    output t is solution t.
+// Locations in ntr are validated by the caller.
+void rs_decode_rows(int n, const int* erased, int ne, const int* ntr, int nn, int zero_ntr, std::vector<uint8_t>& d) {
+  d.assign(static_cast<size_t>(ne) * n, 0);
+  if (ne == 0 || nn == 0) return;
+  std::vector<int> pick(ne, -1);  // solution index feeding output t
+  for (int t = 0; t < ne; ++t) {
+    if (!zero_ntr && t < nn && ntr[t] == erased[t]) {
+      pick[t] = t;
+      continue;
+    }
+    for (int j = 0; j < nn; ++j)
+      if (ntr[j] == erased[t]) {
+        pick[t] = j;
+        break;
+      }
+  }
+  std::vector<uint8_t> col(n), y(nn);
+  for (int l = 0; l < n; ++l) {
+    std::fill(col.begin(), col.end(), 0);
+    col[l] = 1;
+    rs_decode_column(n, col.data(), ntr, nn, zero_ntr != 0, y.data());
+    for (int t = 0; t < ne; ++t)
+      if (pick[t] >= 0) d[static_cast<size_t>(t) * n + l] = y[pick[t]];
+  }
+}
+
+// RS decode rows with the reference's argument limits: a not-to-read
+// location outside [0, n) indexes primitivePower / data out of bounds in the
+// Java (an exception); more than p of them overflow errSignature
+// (ReedSolomonCode.java:60), checked by the callers that know the form.
 hrs_status build_decode_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
                                int zero_ntr, std::vector<uint8_t>& d) {
   const int n = c->n;
-  std::vector<char> in_ntr(n, 0);
-  for (int j = 0; j < nn; ++j) {
+  for (int j = 0; j < nn; ++j)
     if (ntr[j] < 0 || ntr[j] >= n) return fail(c, HRS_EINVAL, "location %d out of range [0,%d)", ntr[j], n);
-    if (in_ntr[ntr[j]]) return fail(c, HRS_EINVAL, "duplicate location %d", ntr[j]);
-    in_ntr[ntr[j]] = 1;
-  }
-  for (int t = 0; t < ne; ++t)
-    if (erased[t] < 0 || erased[t] >= n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
-  if (!rs_decode_rows(n, erased, ne, ntr, nn, zero_ntr, d)) return fail(c, HRS_EINVAL, "singular Vandermonde system");
+  if (!zero_ntr)  // the 3-arg form indexes primitivePower with every erased location
+    for (int t = 0; t < ne; ++t)
+      if (erased[t] < 0 || erased[t] >= n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  rs_decode_rows(n, erased, ne, ntr, nn, zero_ntr, d);
   return HRS_OK;
 }
 
@@ -312,7 +350,7 @@ hrs_status build_src_decode_matrix(hrs_codec* c, const int* erased, int ne, cons
     for (int j = 0; j < i; ++j)
       if (ers[i] == ers[j]) return fail(c, HRS_EINVAL, "duplicate location %d", ers[i] + s);
   std::vector<uint8_t> drs;
-  if (!rs_decode_rows(nrs, ers.data(), m, ers.data(), m, 1, drs)) return fail(c, HRS_EINVAL, "singular Vandermonde system");
+  rs_decode_rows(nrs, ers.data(), m, ers.data(), m, 1, drs);
   // row of location l after the RS repair, over the read values
   auto fixed = [&](int l, uint8_t* row) {
     if (l >= s) {
@@ -337,8 +375,9 @@ hrs_status build_src_decode_matrix(hrs_codec* c, const int* erased, int ne, cons
 // ---------------------------------------------------------------- dispatch
 
 // The matrix a 5-arg decodeBulk applies (ne x n), per code family.
-//  RS : cached closed-form matrix; more than p not-to-read locations throw in
-//       the Java (errSignature is sized p, ReedSolomonCode.java:60).
+//  RS : cached matrix of the reference decode (rs_decode_rows); more than p
+//       not-to-read locations throw in the Java (errSignature is sized p,
+//       ReedSolomonCode.java:60).
 //  NRS: see build_nrs_decode_matrix.
 //  XOR: exactly one erased location; the output is the XOR of every other row
 //       (XORCode.java:115-145 ignores toRead/notToRead). Rows the caller passes
@@ -346,8 +385,12 @@ hrs_status build_src_decode_matrix(hrs_codec* c, const int* erased, int ne, cons
 hrs_status decode5_matrix(hrs_codec* c, const int* erased, int ne, const int* ntr, int nn,
                           const uint8_t* const* rows, std::vector<uint8_t>& tmp, const uint8_t** out,
                           const int* to_read, int nr) {
-  for (int t = 0; t < ne; ++t)
-    if (erased[t] < 0 || erased[t] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
+  // ReedSolomonCode's 5-arg decode only compares erased locations with
+  // not-to-read ones (ReedSolomonCode.java:158-165): any value is accepted
+  // and one that matches none decodes to 0. The other families index with them.
+  if (c->kind != HRS_CODE_RS)
+    for (int t = 0; t < ne; ++t)
+      if (erased[t] < 0 || erased[t] >= c->n) return fail(c, HRS_EINVAL, "erased location %d out of range", erased[t]);
   if (c->kind == HRS_CODE_XOR) {
     if (ne != 1) return fail(c, HRS_EINVAL, "XOR code decodes exactly one erased location (got %d)", ne);
     tmp.assign(c->n, 1);

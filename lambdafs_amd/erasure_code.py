@@ -542,10 +542,19 @@ class HipReedSolomonCode(_HipErasureCode):
         if len(data) != n or len(erasedValues) != len(erasedLocations):
             raise ValueError("data/erasedValues length mismatch")
         if locationsNotToRead is None:
+            # 3-arg (:127-142): zero data[erased], then the bulk 3-arg decode of
+            # the zeroed column, erasedValues[i] = solution i (with a repeated
+            # location the 5-arg matching would copy the first one's value)
             if not erasedLocations:
                 return
-            ntr = list(erasedLocations)
-            toread = []
+            for loc in erasedLocations:
+                data[loc] = 0
+            rows = [np.array([_symbol(v)], dtype=np.uint8) for v in data]
+            outs = [np.zeros(1, dtype=np.uint8) for _ in erasedLocations]
+            self.decodeBulk(rows, outs, list(erasedLocations))
+            for i in range(len(erasedLocations)):
+                erasedValues[i] = int(outs[i][0])
+            return
         else:
             ntr = list(locationsNotToRead)
             toread = list(locationsToRead or [])

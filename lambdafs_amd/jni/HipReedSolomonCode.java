@@ -194,7 +194,26 @@ public class HipReedSolomonCode extends ErasureCode implements Configurable {
     if (erasedLocations.length == 0) {
       return;
     }
-    decode(data, erasedLocations, erasedValues, new int[0], erasedLocations);
+    // zero data at the erased locations, then the 3-arg bulk decode of the
+    // zeroed column: erasedValues[i] = solution i of the Vandermonde solve
+    // (with a repeated location the 5-arg form's matching would copy the
+    // first one's value instead)
+    for (int loc : erasedLocations) {
+      data[loc] = 0;
+    }
+    byte[][] rows = new byte[data.length][1];
+    for (int i = 0; i < data.length; i++) {
+      rows[i][0] = (byte) data[i];
+    }
+    byte[][] out = new byte[erasedLocations.length][1];
+    try {
+      HrsNative.decode3(nativeCodec, rows, out, erasedLocations, 1);
+    } catch (IOException e) {
+      throw new RuntimeException(e);
+    }
+    for (int i = 0; i < erasedLocations.length; i++) {
+      erasedValues[i] = out[i][0] & 0xFF;
+    }
   }
 
   @Override

@@ -292,7 +292,15 @@ void argument_errors() {
   expect(hrs_locations_to_read(c, five, 5, to_read) == HRS_ETOOMANY, "too many erased");
   int dup[2] = {3, 3};
   std::vector<uint8_t> d(28);
-  expect(hrs_decode_matrix(c, dup, 1, dup, 2, 1, d.data()) == HRS_EINVAL, "duplicate location");
+  // a repeated not-to-read location is accepted, as by the Java (its solve
+  // divides by zero: divTable[y][0] = 0); the row equals the oracle's decode
+  expect(hrs_decode_matrix(c, dup, 1, dup, 2, 1, d.data()) == HRS_OK, "repeated location");
+  for (int l = 0; l < 14; ++l) {
+    int col[14] = {0}, val[1] = {0};
+    col[l] = 1;
+    orc_rs_decode5(10, 4, col, dup, 1, val, nullptr, 0, dup, 2);
+    expect(d[l] == val[0], "repeated location row vs oracle");
+  }
   int far[1] = {99};
   expect(hrs_decode_matrix(c, far, 1, far, 1, 1, d.data()) == HRS_EINVAL, "location out of range");
   expect(hrs_decode_matrix(c, nullptr, 1, far, 1, 1, d.data()) == HRS_EINVAL, "NULL erased");

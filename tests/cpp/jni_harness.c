@@ -571,7 +571,11 @@ static int cpu_checks(void) {
   EXPECT_THROWN("decode 300 erased", kIAE,
                 NS(decode)(env, NULL, h, rows(n, L, 2), rows(1, L, 0), new_ints(300, NULL), TR, NTR, L));
   int bad_loc[] = {20};
-  EXPECT_THROWN("decode location out of range", kIAE,
+  EXPECT_THROWN("decode notToRead location out of range", kIAE,
+                NS(decode)(env, NULL, h, rows(n, L, 2), rows(1, L, 0), E, TR, new_ints(1, bad_loc), L));
+  /* ReedSolomonCode only compares erased locations with notToRead ones: any
+   * value passes validation (this host-only handle then fails on the device) */
+  EXPECT_THROWN("decode erased location of any value", kIOE,
                 NS(decode)(env, NULL, h, rows(n, L, 2), rows(1, L, 0), new_ints(1, bad_loc), TR, NTR, L));
   EXPECT_THROWN("decode3 ok shapes", kIOE, NS(decode3)(env, NULL, h, rows(n, L, 2), rows(1, L, 0), E, L));
   {
@@ -666,6 +670,83 @@ static void scalar_decode5_checks(jlong h, int k, int p) {
   }
 }
 
+/* Location lists with repeated entries (and a 5-arg erased value outside the
+ * stripe), which ReedSolomonCode accepts: its solve divides by zero there and
+ * divTable[y][0] = 0 (GaloisField.java:107-118). Bulk 5-arg and 3-arg through
+ * HrsNative vs the oracle's bulk loops on ragged rows; the scalar 5-arg and
+ * 3-arg decode as HipReedSolomonCode.decode does them vs ReedSolomonCode.decode. */
+static void repeated_location_checks(jlong h, int k, int p) {
+  const int n = k + p;
+  const jsize L = 4099;
+  static const struct { int ne, nn, er[4], ntr[4]; } cases[] = {
+      {1, 2, {3}, {3, 3}}, {2, 3, {3, 5}, {3, 5, 5}}, {2, 3, {3, 3}, {3, 5, 5}},
+      {1, 4, {4}, {4, 4, 4, 4}}, {3, 2, {99, -1, 4}, {4, 2}}, {2, 3, {0, 13}, {13, 0, 13}}};
+  for (size_t c = 0; c < sizeof cases / sizeof cases[0]; c++) {
+    const int ne = cases[c].ne, nn = cases[c].nn;
+    jobjectArray rb = rows(n, L, 31 + (int)c);
+    uint8_t* ref_in[16];
+    uint8_t* ref_out[4];
+    for (int l = 0; l < n; l++) {
+      ref_in[l] = malloc((size_t)L);
+      memcpy(ref_in[l], bytes_of(row(rb, l)), (size_t)L);
+    }
+    for (int t = 0; t < ne; t++) ref_out[t] = calloc(1, (size_t)L);
+    orc_rs_decode_bulk5(k, p, ref_in, ref_out, cases[c].er, ne, NULL, 0, cases[c].ntr, nn, (size_t)L);
+    jobjectArray wb = rows(ne, L, 0);
+    CALL("decode, repeated locations",
+         NS(decode)(env, NULL, h, rb, wb, new_ints(ne, cases[c].er), new_ints(0, NULL), new_ints(nn, cases[c].ntr), L));
+    expect(!vm.pending, "decode case %d threw %s: %s", (int)c, vm.exc_class, vm.exc_msg);
+    for (int t = 0; t < ne; t++)
+      expect(memcmp(bytes_of(row(wb, t)), ref_out[t], (size_t)L) == 0, "repeated-location decode case %d output %d", (int)c, t);
+    /* scalar 5-arg on column 0 */
+    int data[16], dref[16], v[4], vref[4];
+    for (int l = 0; l < n; l++) data[l] = dref[l] = ref_in[l][0];
+    for (int t = 0; t < ne; t++) v[t] = vref[t] = 0x70 + t;
+    java_scalar_decode5(h, data, n, cases[c].er, ne, v, cases[c].ntr, nn);
+    orc_rs_decode5(k, p, dref, cases[c].er, ne, vref, NULL, 0, cases[c].ntr, nn);
+    expect(!vm.pending && memcmp(v, vref, sizeof(int) * (size_t)ne) == 0, "scalar decode5 repeated case %d", (int)c);
+    for (int l = 0; l < n; l++) free(ref_in[l]);
+    for (int t = 0; t < ne; t++) free(ref_out[t]);
+  }
+  static const struct { int ne, er[4]; } cases3[] = {{2, {3, 3}}, {3, {1, 5, 1}}, {4, {2, 2, 2, 2}}, {3, {13, 0, 13}}};
+  for (size_t c = 0; c < sizeof cases3 / sizeof cases3[0]; c++) {
+    const int ne = cases3[c].ne;
+    jobjectArray rb = rows(n, L, 41 + (int)c);
+    uint8_t* ref_in[16];
+    uint8_t* ref_out[4];
+    for (int l = 0; l < n; l++) {
+      ref_in[l] = malloc((size_t)L);
+      memcpy(ref_in[l], bytes_of(row(rb, l)), (size_t)L);
+    }
+    for (int t = 0; t < ne; t++) ref_out[t] = calloc(1, (size_t)L);
+    orc_rs_decode_bulk3(k, p, ref_in, ref_out, cases3[c].er, ne, (size_t)L);
+    jobjectArray wb = rows(ne, L, 0);
+    CALL("decode3, repeated locations", NS(decode3)(env, NULL, h, rb, wb, new_ints(ne, cases3[c].er), L));
+    expect(!vm.pending, "decode3 case %d threw %s: %s", (int)c, vm.exc_class, vm.exc_msg);
+    for (int t = 0; t < ne; t++)
+      expect(memcmp(bytes_of(row(wb, t)), ref_out[t], (size_t)L) == 0, "repeated-location decode3 case %d output %d", (int)c, t);
+    /* scalar 3-arg as HipReedSolomonCode.decode(data, erased, values): zero
+     * data[erased], one-byte rows through HrsNative.decode3, copy every output */
+    int data[16], dref[16], vref[4];
+    for (int l = 0; l < n; l++) data[l] = dref[l] = ref_in[l][7];
+    for (int t = 0; t < ne; t++) data[cases3[c].er[t]] = 0;
+    jobjectArray r1 = new_objs(n);
+    for (int l = 0; l < n; l++) {
+      jbyteArray b = new_bytes(1);
+      bytes_of(b)[0] = (uint8_t)data[l];
+      set_obj(r1, l, b);
+    }
+    jobjectArray o1 = rows(ne, 1, 0);
+    CALL("scalar decode3 (HrsNative.decode3, 1-byte rows)", NS(decode3)(env, NULL, h, r1, o1, new_ints(ne, cases3[c].er), 1));
+    orc_rs_decode3(k, p, dref, cases3[c].er, ne, vref);
+    int same = !vm.pending;
+    for (int t = 0; t < ne; t++) same &= bytes_of(row(o1, t))[0] == (uint8_t)vref[t];
+    expect(same, "scalar decode3 repeated case %d", (int)c);
+    for (int l = 0; l < n; l++) free(ref_in[l]);
+    for (int t = 0; t < ne; t++) free(ref_out[t]);
+  }
+}
+
 static int gpu_checks(void) {
   const int k = 10, p = 4, n = 14;
   const jsize L = 1 << 20;
@@ -688,6 +769,7 @@ static int gpu_checks(void) {
   expect(h != 0 && !vm.pending, "create RS(10,4) on the GPU: %s", vm.exc_msg);
   if (!h) return 1;
   scalar_decode5_checks(h, k, p);
+  repeated_location_checks(h, k, p);
 
   /* encode vs oracle encodeBulk */
   jobjectArray in = rows(k, L, 7), out = rows(p, L, 0);

@@ -114,6 +114,68 @@ def test_decode3_matrix_matches_oracle():
             assert list(D[:, col]) == [int(o[0]) for o in out]
 
 
+REPEATED5 = [([3], [3, 3]), ([3, 5], [3, 5, 5]), ([3, 3], [3, 5, 5]), ([3, 3], [3, 3]), ([4], [4, 4, 4, 4]),
+             ([0, 13], [13, 0, 13]), ([7, 7, 7], [1, 7, 7, 2]), ([99, -1, 4], [4, 2]), ([5, 5], [])]
+REPEATED3 = [[3, 3], [1, 5, 1], [2, 2, 2, 2], [13, 0, 13]]
+
+
+def _gf_apply(D, rows):
+    """out_t = XOR_l D[t][l] * rows[l] over GF(2^8), through the oracle's tables."""
+    from oracle import rs_ref
+    mul = np.array(rs_ref.MUL, dtype=np.uint8)
+    out = np.zeros((D.shape[0], rows.shape[1]), dtype=np.uint8)
+    for t in range(D.shape[0]):
+        for l in range(D.shape[1]):
+            if D[t, l]:
+                out[t] ^= mul[D[t, l]][rows[l]]
+    return out
+
+
+@pytest.mark.parametrize("k,p", [(10, 4), (6, 3)])
+def test_decode_matrix_repeated_locations_match_java(k, p):
+    """VERDICT r5 missing #3: lists the Java accepts with repeated entries (a
+    division by zero in solveVandermondeSystem is divTable[y][0] = 0,
+    GaloisField.java:107-118) and, in the 5-arg form, erased locations of any
+    value (ReedSolomonCode.java:158-165 only compares them). The matrix must
+    reproduce the reference's per-byte bulk loops on arbitrary bytes."""
+    n = k + p
+    code = HipReedSolomonCode(k, p, device=NONE)
+    rng = np.random.default_rng(k * 100 + p)
+    rows = rng.integers(0, 256, (n, 257), dtype=np.uint8)
+    for erased, ntr in REPEATED5:
+        ntr = [x for x in ntr if x < n]
+        D = code.decodeMatrix(erased, ntr)
+        want = C.decode_bulk5(k, p, [r.copy() for r in rows], erased, [], ntr)
+        assert (_gf_apply(D, rows) == np.array(want)).all(), (erased, ntr)
+        assert (D == _probe_decode5(k, p, erased, [], ntr)).all(), (erased, ntr)
+    for erased in REPEATED3:
+        erased = [x for x in erased if x < n]
+        D = code.decodeMatrix(erased, erased, zero_not_to_read=False)
+        want = C.decode_bulk3(k, p, [r.copy() for r in rows], erased)
+        assert (_gf_apply(D, rows) == np.array(want)).all(), erased
+
+
+def test_decode_matrix_repeated_two_transcriptions():
+    """The C oracle and the independent Python transcription agree on the
+    repeated-location cases the engine now accepts (pins the oracle there)."""
+    from oracle.rs_ref import ReedSolomonRef
+    k, p = 10, 4
+    ref = ReedSolomonRef(k, p)
+    rng = np.random.default_rng(7)
+    data = [int(v) for v in rng.integers(0, 256, k + p)]
+    for erased, ntr in REPEATED5:
+        assert ref.decode5(list(data), erased, [], ntr) == C.decode5(k, p, list(data), erased, [], ntr), (erased, ntr)
+
+
+def test_decode_matrix_rejects_what_java_rejects():
+    """A not-to-read location outside [0, n) throws in the Java
+    (primitivePower / data index); so does a 3-arg erased one."""
+    code = HipReedSolomonCode(10, 4, device=NONE)
+    for erased, ntr, zero in [([3], [14], True), ([3], [-1], True), ([14], [14], False), ([-1], [-1], False)]:
+        with pytest.raises(HrsError):
+            code.decodeMatrix(erased, ntr, zero_not_to_read=zero)
+
+
 def test_locations_to_read_matches_java():
     code = HipReedSolomonCode(10, 4, device=NONE)
     lib = _lib.lib()
@@ -135,14 +197,6 @@ def test_create_rejects_bad_geometry():
             HipReedSolomonCode(k, p, device=NONE)
         assert ei.value.status == _lib.HRS_EINVAL
     assert HipReedSolomonCode(254, 1, device=NONE).stripeSize() == 254
-
-
-def test_decode_matrix_rejects_duplicates_and_range():
-    code = HipReedSolomonCode(10, 4, device=NONE)
-    with pytest.raises(HrsError):
-        code.decodeMatrix([4], [4, 4])
-    with pytest.raises(HrsError):
-        code.decodeMatrix([14], [1])
 
 
 def test_host_only_handle_refuses_coding():

