@@ -20,23 +20,15 @@ API_OBJ  := $(patsubst %,build/%.o,$(API_SRC))
 
 JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
-            tests/cpp/copy_pool_test tests/cpp/page_claims_test
+            tests/cpp/copy_pool_test
 
-TOOLS    := tools/host_call_rate tools/register_zc_probe tools/register_par_probe
+TOOLS    := tools/host_call_rate
 
 all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
 
 # The synchronous C-ABI call rate (bench.py's host_calls leg, profiles/r05/).
 tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
-
-# Staged vs page-registered synchronous calls (profiles/r05/NOTES.md).
-tools/register_zc_probe: tools/register_zc_probe.cpp include/hrs.h $(LIB)
-	$(HIPCC) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
-
-# Serial vs multi-threaded registration of a call's rows (profiles/r05/NOTES.md).
-tools/register_par_probe: tools/register_par_probe.cpp
-	$(HIPCC) -O2 -std=c++17 -Wall -pthread -o $@ $<
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build
@@ -76,7 +68,8 @@ build/hrs_probe.o: lambdafs_amd/csrc/hrs_probe.hip include/hrs_probe.h $(HDRS)
 KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_decode_crc.o
 
 $(LIB): $(API_OBJ) $(KOBJ) lambdafs_amd/csrc/libhrs.map
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs.map -o $@ $(API_OBJ) $(KOBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs.map -o $@ $(API_OBJ) $(KOBJ) \
+	    -L/opt/rocm/lib -lhsa-runtime64
 
 # HBM ceiling probes (include/hrs_probe.h): a side library for bench.py and
 # tools only; the product libhrs.so does not carry diagnostics.
@@ -116,10 +109,6 @@ tests/cpp/crc_tables: tests/cpp/crc_tables.cpp lambdafs_amd/csrc/crc32.hpp lambd
 tests/cpp/copy_pool_test: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
 	g++ -O2 -std=c++17 -Wall -pthread -o $@ $<
 
-# The direct calls' process-wide page claims under concurrent holders (CPU only).
-tests/cpp/page_claims_test: tests/cpp/page_claims_test.cpp lambdafs_amd/csrc/hrs_host.hpp
-	g++ -O2 -std=c++17 -Wall -pthread -o $@ $<
-
 tests/cpp/crc_model: tests/cpp/crc_model.cpp lambdafs_amd/csrc/crc32.hpp
 	g++ -O2 -std=c++17 -Wall -o $@ $< -lz
 
@@ -134,7 +123,7 @@ SAN      := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-om
 HSAN     := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
             -Xarch_host -fno-omit-frame-pointer
 ASAN_BIN := $(ASAN_DIR)/host_logic $(ASAN_DIR)/jni_harness $(ASAN_DIR)/codec_harness
-ASAN_LOG := profiles/r05/asan
+ASAN_LOG := profiles/r06/asan
 
 ASAN_API := $(patsubst %,$(ASAN_DIR)/%.o,$(API_SRC))
 $(ASAN_API): $(ASAN_DIR)/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
@@ -174,12 +163,11 @@ asan: $(ASAN_BIN)
 
 # ---- make tsan: the host copy pool (hrs_host.hpp: concurrent callers,
 # spinning workers that drain the batches they join) under ThreadSanitizer.
-TSAN_LOG := profiles/r05/tsan
-tsan: tests/cpp/copy_pool_test.cpp tests/cpp/page_claims_test.cpp lambdafs_amd/csrc/hrs_host.hpp
+TSAN_LOG := profiles/r06/tsan
+tsan: tests/cpp/copy_pool_test.cpp lambdafs_amd/csrc/hrs_host.hpp
 	@mkdir -p build/tsan $(TSAN_LOG)
 	g++ -O1 -g -std=c++17 -fsanitize=thread -pthread -o build/tsan/copy_pool_test tests/cpp/copy_pool_test.cpp
-	g++ -O1 -g -std=c++17 -fsanitize=thread -pthread -o build/tsan/page_claims_test tests/cpp/page_claims_test.cpp
-	sh -c 'for t in 0 1 4 8; do HRS_HOST_THREADS=$$t build/tsan/copy_pool_test 4 20; done; build/tsan/page_claims_test 8 5000' > $(TSAN_LOG)/tsan_run.log 2>&1 || { cat $(TSAN_LOG)/tsan_run.log; exit 1; }
+	sh -c 'for t in 0 1 4 8; do HRS_HOST_THREADS=$$t build/tsan/copy_pool_test 4 20; done' > $(TSAN_LOG)/tsan_run.log 2>&1 || { cat $(TSAN_LOG)/tsan_run.log; exit 1; }
 	@cat $(TSAN_LOG)/tsan_run.log
 
 clean:

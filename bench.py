@@ -466,8 +466,8 @@ def e2e_config5(local, rank, world, golden, S=512, L=256 << 10, reps=3):
     idx = np.arange(S)[:, None]
     dec_ok = bool(np.array_equal(outn, stn[idx, er]))
     mine = SD.stripe_digests(lambda a, b: outn[a:b], S, g0)
-    # pageable host memory: the call registers the batch's whole pages for
-    # its duration ("direct"; HRS_HOST_DIRECT=0: staged through pinned slots)
+    # pageable host memory: staged through the handle's pinned slots (the
+    # GPU never writes into memory the runtime did not allocate pinned)
     pg = np.array(stn)
     pout = np.zeros((S, 2, L), np.uint8)
     pg_ms = timed(lambda: device.decode_batch_host(code, pg, er, pout))

@@ -195,7 +195,6 @@ void hrs_destroy(hrs_codec* c) {
     if (h.dev) (void)hipFree(h.dev);
     if (h.pin) (void)hipHostFree(h.pin);
   }
-  if (c->direct_raw) (void)hipFree(c->direct_raw);
   for (auto& a : c->async) {
     if (a.stream) {
       (void)hipStreamSynchronize(a.stream);

@@ -4,6 +4,8 @@
 // chunks of stripes through a ring of device slots, H2D of exactly the rows
 // read, D2H of exactly the rows written).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -196,14 +198,30 @@ hrs_status upload_batch_plans(hrs_codec* c, const BatchPlanSet& ps, hipStream_t 
 // the host waits once; pageable ones go through each slot's pinned staging
 // (copy pool), the host then waits for a slot before refilling it.
 
-bool is_pinned(const void* p) {
+// Host memory the runtime allocated pinned, [p, p + len) inside one
+// allocation: hipHostMalloc'd (torch pin_memory included) is an HSA pool
+// allocation whose pages the driver holds for the allocation's lifetime.
+// The GPU reads and writes only such memory in place (zero copy, or DMA by
+// the copy engines). Pageable memory the caller registered with
+// hipHostRegister reports HSA_EXT_POINTER_TYPE_LOCKED: the registration maps
+// its pages for the GPU without pinning them, and a page that moves while a
+// kernel writes it loses the writes into the freed old page (round 5: 5 of 11
+// long fuzz runs; DESIGN.md §7 "Platform constraint"). It is staged like any
+// pageable memory. So is device memory (HSA type too, but not host memory).
+bool runtime_pinned(const void* p, size_t len) {
   if (!p) return false;
   hipPointerAttribute_t attr{};
   if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory is reported as an error: clear it
     return false;
   }
-  return attr.type == hipMemoryTypeHost;
+  if (attr.type != hipMemoryTypeHost) return false;
+  hsa_amd_pointer_info_t info{};
+  info.size = sizeof info;
+  if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
+  if (info.type != HSA_EXT_POINTER_TYPE_HSA || !info.hostBaseAddress) return false;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(info.hostBaseAddress), a = reinterpret_cast<uintptr_t>(p);
+  return a >= b && len <= info.sizeInBytes && a - b <= info.sizeInBytes - len;
 }
 
 bool zero_copy_on() {
@@ -225,9 +243,9 @@ unsigned zero_copy_blocks() {
 // (HIP's unified addressing on these systems): then any pointer into a pinned
 // allocation, base or interior, is valid in a kernel as it stands, with no
 // question of how an interior pointer's offset maps. Anything else (pageable
-// memory, another mapping) takes the copy engine.
-bool host_device_ptr(const void* p, uint8_t** dp) {
-  if (!p || !is_pinned(p)) return false;
+// or caller-registered memory, another mapping) is staged.
+bool host_device_ptr(const void* p, size_t len, uint8_t** dp) {
+  if (!p || !runtime_pinned(p, len)) return false;
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
     (void)hipGetLastError();
@@ -236,6 +254,11 @@ bool host_device_ptr(const void* p, uint8_t** dp) {
   if (d != p) return false;
   *dp = static_cast<uint8_t*>(d);
   return true;
+}
+
+// Bytes a strided batch spans from its base: the last stripe's last row end.
+size_t batch_span(size_t nstripes, size_t stripe_stride, int rows, size_t row_stride, size_t len) {
+  return (nstripes - 1) * stripe_stride + static_cast<size_t>(rows - 1) * row_stride + len;
 }
 
 size_t hbatch_target_bytes() {
@@ -292,7 +315,7 @@ hrs_status hbatch_slot(hrs_codec* c, int i, size_t dev_bytes, size_t pin_bytes) 
     h.pin_bytes = 0;
     hipError_t e = hipHostMalloc(&h.pin, pin_bytes, hipHostMallocDefault);
     if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", pin_bytes, hipGetErrorString(e));
-    if (!host_device_ptr(h.pin, &h.pin_dev)) h.pin_dev = nullptr;
+    if (!host_device_ptr(h.pin, pin_bytes, &h.pin_dev)) h.pin_dev = nullptr;
     h.pin_bytes = pin_bytes;
   }
   return HRS_OK;
@@ -355,7 +378,8 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
   const size_t out_stripe_dev = dpitch * static_cast<size_t>(out_rows_max);
   size_t chunk = std::max<size_t>(1, hbatch_target_bytes() / std::max<size_t>(1, img_stripe));
   chunk = std::min(chunk, nstripes);
-  const bool pinned = is_pinned(hin) && is_pinned(hout);
+  const bool pinned = runtime_pinned(hin, batch_span(nstripes, in_stripe, img_rows, in_row, len)) &&
+                      runtime_pinned(hout, batch_span(nstripes, out_stripe, out_rows_max, out_row, len));
   const size_t dev_bytes = chunk * (img_stripe + out_stripe_dev);
   const size_t pin_bytes = pinned ? 0 : dev_bytes;  // staging mirrors the device image
   // pageable callers, zero copy: the kernels read each chunk's image from the
@@ -586,27 +610,11 @@ using namespace hrs::api;
 
 namespace {
 
-// hrs_last_host_path of a batch that was not registered for the call.
-const char* batch_path(const void* in, const void* out) {
-  uint8_t* d = nullptr;
+// hrs_last_host_path of a host batch: "pinned" when the stripes (and a
+// decode's outputs) lie in runtime-pinned memory and zero copy is on.
+const char* batch_path(bool pinned) {
   if (!zero_copy_on()) return "copy_engine";
-  return host_device_ptr(in, &d) && host_device_ptr(out, &d) ? "pinned" : "staged";
-}
-
-// Pageable host batches straight over the caller's memory (round 5, as the
-// synchronous calls: hrs_hostpath.cpp host_apply_direct). The whole pages
-// inside the batch's spans (stripes, and the outputs of a decode) are
-// registered for the call (RegisteredPages); the stripes that lie inside them
-// take the zero-copy batch path as if the caller had pinned them, and the few
-// stripes at either end that reach into a partial page take the staged path
-// after. tools/register_batch_probe.py, config 5's repair (512 x RS(12,4),
-// 256 KiB cells, 2.4 GB): registration 0.1-4.6 ms + 28.5 ms vs 37.6-38.1 ms
-// staged. Taken when zero copy is on, HRS_HOST_DIRECT is not 0, the buffers
-// are pageable, the inner stripes span at least host_direct_min and every
-// claim and registration succeeds; otherwise the whole batch is staged.
-bool batch_direct_candidate(const void* p) {
-  uint8_t* d = nullptr;
-  return host_direct_on() && zero_copy_on() && !host_device_ptr(p, &d);
+  return pinned ? "pinned" : "staged";
 }
 
 hrs_status decode_batch_host_impl(hrs_codec* c, const uint8_t* stripes, size_t row_stride, size_t stripe_stride,
@@ -624,7 +632,8 @@ hrs_status decode_batch_host_impl(hrs_codec* c, const uint8_t* stripes, size_t r
   DeviceGuard g(c->device);
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   uint8_t *zs = nullptr, *zo = nullptr;
-  if (zero_copy_on() && host_device_ptr(stripes, &zs) && host_device_ptr(out, &zo))
+  if (zero_copy_on() && host_device_ptr(stripes, batch_span(nstripes, stripe_stride, c->n, row_stride, len), &zs) &&
+      host_device_ptr(out, batch_span(nstripes, out_stripe_stride, max_erased, out_row_stride, len), &zo))
     return drain_hbatch(c, zero_copy_batch(c, ps, zs, row_stride, stripe_stride, zo, out_row_stride,
                                            out_stripe_stride, len, nstripes));
   // rows each pattern reads: its live locations (every location for the
@@ -689,7 +698,8 @@ hrs_status encode_batch_host_impl(hrs_codec* c, uint8_t* stripes, size_t row_str
   if (!g.ok) return fail(c, HRS_EDEVICE, "cannot select HIP device %d", c->device);
   const int k = c->k, p = c->p;
   uint8_t* zs = nullptr;
-  if (zero_copy_on() && host_device_ptr(stripes, &zs)) {  // pinned: the kernel works on the caller's stripes
+  if (zero_copy_on() && host_device_ptr(stripes, batch_span(nstripes, stripe_stride, c->n, row_stride, len), &zs)) {
+    // runtime-pinned: the kernel works on the caller's stripes in place
     hrs_status st = hbatch_slot(c, 0, 0, 0);
     if (st != HRS_OK) return st;
     const hipStream_t hs = c->hbatch[0].stream;
@@ -769,40 +779,14 @@ hrs_status hrs_decode_batch_host(hrs_codec* c, const uint8_t* stripes, size_t ro
     return fail(c, HRS_EINVAL, "bad batch decode arguments (max_erased must be in [0, %d])", hrs::kMaxOut);
   if (nstripes == 0 || len == 0 || max_erased == 0) return HRS_OK;
   if (nstripes > 0x7fffffffu) return fail(c, HRS_EINVAL, "too many stripes");
-  {  // every pattern is checked before any stripe is touched (the direct path splits the batch)
-    BatchPlanSet ps;
-    const hrs_status st = build_batch_plans(c, erased, max_erased, nstripes, ps);
-    if (st != HRS_OK) return st;
-  }
-  DeviceGuard g(c->device);  // a registration maps the pages for the codec's device
-  if (g.ok && batch_direct_candidate(stripes) && batch_direct_candidate(out)) {
-    const hrs::InnerStripes a = hrs::inner_stripes(stripes, stripe_stride, (c->n - 1) * row_stride + len, nstripes);
-    const size_t out_ext = static_cast<size_t>(max_erased - 1) * out_row_stride + len;
-    const hrs::InnerStripes b = hrs::inner_stripes(out, out_stripe_stride, out_ext, nstripes);
-    const size_t lo = std::max(a.lo, b.lo), hi = std::min(a.hi, b.hi);
-    if (hi > lo && (hi - lo) * stripe_stride >= host_direct_min(false)) {
-      RegisteredPages reg({{a.p0, a.p1}, {b.p0, b.p1}});
-      if (reg.ok()) {
-        const size_t me = static_cast<size_t>(max_erased);
-        hrs_status st = decode_batch_host_impl(c, stripes + lo * stripe_stride, row_stride, stripe_stride,
-                                               erased + lo * me, max_erased, out + lo * out_stripe_stride,
-                                               out_row_stride, out_stripe_stride, len, hi - lo);
-        reg.release();  // the call has synchronized
-        if (st == HRS_OK && lo > 0)
-          st = decode_batch_host_impl(c, stripes, row_stride, stripe_stride, erased, max_erased, out, out_row_stride,
-                                      out_stripe_stride, len, lo);
-        if (st == HRS_OK && hi < nstripes)
-          st = decode_batch_host_impl(c, stripes + hi * stripe_stride, row_stride, stripe_stride, erased + hi * me,
-                                      max_erased, out + hi * out_stripe_stride, out_row_stride, out_stripe_stride,
-                                      len, nstripes - hi);
-        c->last_host_path = "direct";
-        return st;
-      }
-    }
-  }
   const hrs_status st = decode_batch_host_impl(c, stripes, row_stride, stripe_stride, erased, max_erased, out,
                                                out_row_stride, out_stripe_stride, len, nstripes);
-  c->last_host_path = batch_path(stripes, out);
+  if (st == HRS_OK) {
+    DeviceGuard g(c->device);
+    c->last_host_path =
+        batch_path(g.ok && runtime_pinned(stripes, batch_span(nstripes, stripe_stride, c->n, row_stride, len)) &&
+                   runtime_pinned(out, batch_span(nstripes, out_stripe_stride, max_erased, out_row_stride, len)));
+  }
   return st;
 }
 
@@ -811,26 +795,12 @@ hrs_status hrs_encode_batch_host(hrs_codec* c, uint8_t* stripes, size_t row_stri
   if (!c) return HRS_EINVAL;
   if (!stripes) return fail(c, HRS_EINVAL, "stripes is NULL");
   if (nstripes == 0 || len == 0) return HRS_OK;
-  DeviceGuard g(c->device);
-  if (g.ok && batch_direct_candidate(stripes)) {
-    const hrs::InnerStripes a = hrs::inner_stripes(stripes, stripe_stride, (c->n - 1) * row_stride + len, nstripes);
-    if (a.hi > a.lo && (a.hi - a.lo) * stripe_stride >= host_direct_min(false)) {
-      RegisteredPages reg({{a.p0, a.p1}});
-      if (reg.ok()) {
-        hrs_status st = encode_batch_host_impl(c, stripes + a.lo * stripe_stride, row_stride, stripe_stride, len,
-                                               a.hi - a.lo);
-        reg.release();
-        if (st == HRS_OK && a.lo > 0) st = encode_batch_host_impl(c, stripes, row_stride, stripe_stride, len, a.lo);
-        if (st == HRS_OK && a.hi < nstripes)
-          st = encode_batch_host_impl(c, stripes + a.hi * stripe_stride, row_stride, stripe_stride, len,
-                                      nstripes - a.hi);
-        c->last_host_path = "direct";
-        return st;
-      }
-    }
-  }
   const hrs_status st = encode_batch_host_impl(c, stripes, row_stride, stripe_stride, len, nstripes);
-  c->last_host_path = batch_path(stripes, stripes);
+  if (st == HRS_OK) {
+    DeviceGuard g(c->device);
+    c->last_host_path =
+        batch_path(g.ok && runtime_pinned(stripes, batch_span(nstripes, stripe_stride, c->n, row_stride, len)));
+  }
   return st;
 }
 

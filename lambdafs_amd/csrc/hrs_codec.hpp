@@ -73,10 +73,6 @@ struct hrs_codec {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
   } host[hrs::kHostSlots];
-  // synchronous calls run straight over the caller's rows (pages registered
-  // for the call, hrs_hostpath.cpp host_apply_direct): raw window-CRC scratch
-  uint32_t* direct_raw = nullptr;
-  size_t direct_raw_bytes = 0;
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
   // its own compute stream; every slot's H2D goes on one copy-in stream and
@@ -119,7 +115,7 @@ struct hrs_codec {
   bool timing = false;  // hrs_set_timing: asynchronous operations record timing events
   std::string err;
   std::string last_kernel;  // main kernel of the latest coding call (hrs_last_kernel)
-  const char* last_host_path = "";  // hrs_last_host_path: "direct" | "staged" | "copy_engine"
+  const char* last_host_path = "";  // hrs_last_host_path: "pinned" | "staged" | "copy_engine"
 };
 
 
@@ -161,38 +157,13 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // call); HRS_ZC_BLOCKS caps the grid of such launches (hrs::GridCap).
 bool zero_copy_on();
 unsigned zero_copy_blocks();
-// Device address of pinned host memory (hipHostMalloc'd or registered), or
-// false for pageable memory.
-bool host_device_ptr(const void* p, uint8_t** dp);
-
-// ---- pageable memory made visible to the GPU for one call (hrs_hostpath.cpp)
-// HRS_HOST_DIRECT=0 turns it off (read per call); host_direct_min: shortest
-// row (or batch span) worth it, plain / checksummed calls.
-bool host_direct_on();
-size_t host_direct_min(bool crc);
-// Host page ranges [first, second) registered with HIP (hipHostRegister,
-// mapped) for the duration of one call. The ranges are sorted and merged
-// (overlapping or touching), claimed process-wide (PageClaims: HIP would
-// accept a page registered twice and then drop it under the other call) and
-// registered. ok() is false, with nothing held, when a claim or registration
-// fails or a device address differs from its host address (zero copy needs
-// them equal). release() (or the destructor) unregisters and drops the
-// claims; every stream that reads the pages must have drained by then.
-class RegisteredPages {
- public:
-  explicit RegisteredPages(std::vector<std::pair<uintptr_t, uintptr_t>> ranges);
-  ~RegisteredPages() { release(); }
-  RegisteredPages(const RegisteredPages&) = delete;
-  RegisteredPages& operator=(const RegisteredPages&) = delete;
-  bool ok() const { return ok_; }
-  void release();
-
- private:
-  std::vector<std::pair<uintptr_t, uintptr_t>> rg_;
-  std::vector<uintptr_t> held_;
-  bool claimed_ = false;
-  bool ok_ = false;
-};
+// Host memory the runtime allocated pinned (hipHostMalloc, torch
+// pin_memory), [p, p + len) inside one allocation. Caller-registered
+// (hipHostRegister) pageable memory is not: its pages can move.
+bool runtime_pinned(const void* p, size_t len);
+// Device address of runtime-pinned host memory [p, p + len) when it equals
+// the host address, or false (pageable or registered memory: staged).
+bool host_device_ptr(const void* p, size_t len, uint8_t** dp);
 
 // The compile-time encode kernels hold the hops RS generator (rs) or the
 // ISA-L Cauchy rows (nrs) of a (k, p) shape; only those families' G may take

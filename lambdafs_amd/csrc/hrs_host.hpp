@@ -12,11 +12,6 @@
 // none is left (a piece per lock round trip cost a 5 MiB copy-in 40-80 us on
 // the MI355X hosts whatever the worker count: tools/pool_probe.cpp). A call
 // returns once all its pieces are copied and no worker still holds its batch.
-//
-// Also the process-wide claims on host page ranges the synchronous calls and
-// pageable host batches register with HIP for their duration (PageClaims,
-// hrs_hostpath.cpp RegisteredPages), and the stripes of a strided batch that
-// lie inside whole pages (inner_stripes, hrs_batch_api.cpp).
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -27,7 +22,6 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
-#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -183,64 +177,5 @@ class CopyPool {
   std::condition_variable cv_, done_cv_;
   bool stop_ = false;
 };
-
-// The page ranges this library holds registered, process-wide. HIP accepts
-// a second hipHostRegister of pageable pages that are already registered, and
-// then the first unregister leaves the second call's kernel without its
-// mapping (and the second unregister aborts in the runtime's memory-object
-// map). Calls on different handles may share input rows (one stripe read by
-// several threads), so a call claims its ranges here first. A range that
-// overlaps one another call holds makes the call take the staged path.
-class PageClaims {
- public:
-  static PageClaims& instance() {
-    static PageClaims p;
-    return p;
-  }
-  bool claim(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (const auto& r : rg) {
-      auto it = held_.lower_bound(r.first);  // first held range starting at or after r.first
-      if (it != held_.end() && it->first < r.second) return false;
-      if (it != held_.begin() && std::prev(it)->second > r.first) return false;
-    }
-    for (const auto& r : rg) held_.emplace(r.first, r.second);
-    return true;
-  }
-  void release(const std::vector<std::pair<uintptr_t, uintptr_t>>& rg) {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (const auto& r : rg) held_.erase(r.first);
-  }
-
- private:
-  std::mutex mu_;
-  std::map<uintptr_t, uintptr_t> held_;  // start -> end, disjoint
-};
-
-struct InnerStripes {
-  size_t lo = 0, hi = 0;  // stripes [lo, hi) lie inside the whole pages [p0, p1)
-  uintptr_t p0 = 0, p1 = 0;
-};
-
-// Stripes of a strided array (stripe s at base + s * stride, `ext` bytes
-// long) that lie inside the whole pages [p0, p1) of the array's span: a
-// contiguous range [lo, hi), empty (hi <= lo) when none does or the stripes
-// overlap (stride < ext).
-inline InnerStripes inner_stripes(const void* base, size_t stride, size_t ext, size_t nstripes) {
-  constexpr uintptr_t kPage = 4096;
-  InnerStripes r;
-  if (nstripes == 0 || ext == 0 || (nstripes > 1 && stride < ext)) return r;  // overlapping stripes: no
-  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-  const uintptr_t end = b + (nstripes - 1) * stride + ext;
-  r.p0 = (b + kPage - 1) & ~(kPage - 1);
-  r.p1 = end & ~(kPage - 1);
-  if (r.p1 <= r.p0) return r;
-  const size_t st = nstripes > 1 ? stride : ext;  // one stripe: its stride is never used
-  r.lo = (r.p0 - b + st - 1) / st;
-  if (r.p1 < b + ext) return r;
-  r.hi = std::min<size_t>(nstripes, (r.p1 - b - ext) / st + 1);
-  if (r.hi < r.lo) r.hi = r.lo;
-  return r;
-}
 
 }  // namespace hrs

@@ -71,7 +71,7 @@ hrs_status host_slot(hrs_codec* c, int i, size_t bytes) {
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   e = hipHostMalloc(&h.pin, bytes, hipHostMallocDefault);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
-  if (!host_device_ptr(h.pin, &h.pin_dev)) h.pin_dev = nullptr;  // then the calls take the copy engine
+  if (!host_device_ptr(h.pin, bytes, &h.pin_dev)) h.pin_dev = nullptr;  // then the calls take the copy engine
   h.bytes = bytes;
   return HRS_OK;
 }
@@ -96,295 +96,17 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
   return it->second;
 }
 
-// ---- synchronous calls straight over the caller's rows (round 5) ----
-// The staged path copies the caller's pageable rows into pinned staging and
-// the outputs back (a 1 MiB-cell RS(10,4) call: 10 MiB in, 4 MiB out, the
-// first copy-in and the last copy-out on the critical path). Instead, the
-// caller's rows are made visible to the GPU for the call and the zero-copy
-// kernel reads the inputs and writes the outputs in place:
-//   - only pages that lie wholly inside a row are registered (RegisteredPages;
-//     ~0.9 us per row, ~0.4 us to unregister), so no page holding anyone
-//     else's bytes is ever registered (a pageable HIP copy by other code that
-//     touched such a page during the call would otherwise fail);
-//   - the columns every row has inside its whole pages, [c0, c1) with c1 - c0
-//     a multiple of 2 KiB, run over the caller's rows; the head [0, c0) and
-//     the tail [c1, len) (each under 4 KiB + 2 KiB) are copied through the
-//     pinned staging and run as ONE small two-stripe launch on a second
-//     stream, beside the middle's (separate head and tail launches, and the
-//     two-pass CRC their ragged widths needed, cost 0.03-0.10 ms per call);
-//   - block CRCs: each of the three column segments yields its own CRC,
-//     chained on the host in column order (CRC32.update);
-//   - the pages are unregistered once the stream has drained.
-// A JVM's 1 MiB byte[] is a G1 humongous object whose data starts 16 bytes
-// past its region start: head 4,080 B, tail 16 B, middle 510 windows.
-// tools/host_call_rate.cpp (profiles/r05/NOTES.md): encode 0.27 ms vs 0.36
-// staged, encode + CRC 0.29 vs 0.38, decode 0.25 vs 0.31.
-// Taken when zero copy is on, every row is 16-byte aligned, len >=
-// host_direct_min (128 KiB, 48 KiB for checksummed calls), the middle spans
-// at least 32 KiB, a checksummed call's middle kernel is one-pass (a
-// two-pass CRC would read the cells across the link twice), no other call of
-// this process holds any of its pages (PageClaims) and every range registers
-// (pages the caller registered fail it). Otherwise the call takes the staged
-// path, with the same results.
-// OFF BY DEFAULT (HRS_HOST_DIRECT=1 turns it on; read per call). A
-// registration maps the caller's pageable pages without pinning them (the
-// driver's userptr objects follow the pages through MMU notifiers), and in
-// long runs of the seeded fuzz suites (tests/tools/fuzz_long.py) a direct call
-// now and then lost the GPU's writes to one page of an output row from one
-// window on: the pattern of a page the kernel moved (THP collapse, compaction)
-// or a stale GPU translation while the kernel ran (profiles/r05/NOTES.md,
-// "Direct path: intermittent lost writes"). Pinned staging
-// (hipHostMalloc'd, never moved) has no such window, so it is the default;
-// the direct path stays for callers whose memory cannot move during a call
-// (hugetlbfs-backed, or a host configured without THP collapse and
-// compaction of unevictable pages).
-bool host_direct_on() {
-  const char* e = getenv("HRS_HOST_DIRECT");
-  return e && e[0] == '1';
-}
-
-// Shortest row the direct path takes: HRS_HOST_DIRECT_MIN for plain calls
-// (default 128 KiB), HRS_HOST_DIRECT_MIN_CRC for checksummed ones (default
-// 48 KiB). Below them the staging copies cost no more than the registrations;
-// a checksummed call gains sooner, as its staged form pays a second launch
-// (profiles/r05/NOTES.md, cell-size sweep).
-size_t env_size(const char* name, size_t dflt) {
-  const char* e = getenv(name);
-  const long x = e ? atol(e) : -1;
-  return x >= 0 ? static_cast<size_t>(x) : dflt;
-}
-
-size_t host_direct_min(bool crc) {
-  static const size_t plain = env_size("HRS_HOST_DIRECT_MIN", static_cast<size_t>(128) << 10);
-  static const size_t with_crc = env_size("HRS_HOST_DIRECT_MIN_CRC", static_cast<size_t>(48) << 10);
-  return crc ? with_crc : plain;
-}
-
-RegisteredPages::RegisteredPages(std::vector<std::pair<uintptr_t, uintptr_t>> ranges) : rg_(std::move(ranges)) {
-  std::sort(rg_.begin(), rg_.end());
-  size_t w = 0;  // merge overlapping and touching ranges: each page is registered once
-  for (size_t r = 1; r < rg_.size(); ++r) {
-    if (rg_[r].first <= rg_[w].second)
-      rg_[w].second = std::max(rg_[w].second, rg_[r].second);
-    else
-      rg_[++w] = rg_[r];
-  }
-  rg_.resize(rg_.empty() ? 0 : w + 1);
-  if (rg_.empty() || !hrs::PageClaims::instance().claim(rg_)) return;  // another call holds some of these pages
-  claimed_ = true;
-  for (const auto& r : rg_) {
-    if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first, hipHostRegisterMapped) != hipSuccess) {
-      (void)hipGetLastError();  // already registered (by the caller), or not registrable
-      release();
-      return;
-    }
-    held_.push_back(r.first);
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(r.first), 0) != hipSuccess ||
-        d != reinterpret_cast<void*>(r.first)) {
-      (void)hipGetLastError();
-      release();
-      return;
-    }
-  }
-  ok_ = true;
-}
-
-void RegisteredPages::release() {
-  for (uintptr_t a : held_) (void)hipHostUnregister(reinterpret_cast<void*>(a));
-  held_.clear();
-  if (claimed_) hrs::PageClaims::instance().release(rg_);
-  claimed_ = false;
-  ok_ = false;
-}
-
-// One direct call at a time per device: a call that finds another one in
-// flight takes the staged path. One direct caller already fills the host
-// link; beside it, the staged callers' host copies overlap its link time,
-// where overlapping direct calls only split the link (and churn
-// registrations): 4 concurrent Encoders 38.8-39.6 GiB/s of user data this
-// way, 31.9-34.9 with direct calls overlapping, 35.3-38.1 all staged
-// (profiles/r05/NOTES.md). HRS_HOST_DIRECT_EXCL=0 lets them overlap (A/B
-// runs; read per call).
-// The turn is per device: each GPU has its own host link, so codecs on
-// different devices (a device set, one Encoder per GPU) go direct side by side.
-constexpr int kTurnSlots = 64;  // devices beyond share the last slot
-std::atomic<int> g_direct_inflight[kTurnSlots];
-struct DirectTurn {
-  bool ok = true;
-  std::atomic<int>& n;
-  explicit DirectTurn(int device) : n(g_direct_inflight[std::min(std::max(device, 0), kTurnSlots - 1)]) {
-    const char* e = getenv("HRS_HOST_DIRECT_EXCL");
-    const int before = n.fetch_add(1);
-    if (!(e && e[0] == '0') && before > 0) ok = false;
-  }
-  ~DirectTurn() { n.fetch_sub(1); }
-  DirectTurn(const DirectTurn&) = delete;
-  DirectTurn& operator=(const DirectTurn&) = delete;
-};
-
-// Runs the call over the caller's rows; false (nothing done, nothing left
-// registered) when the call must take the staged path. *st: its status.
-bool host_apply_direct(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
-                       uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc, int nlive,
-                       hrs_status* st) {
-  if (!host_direct_on() || !zero_copy_on() || len < host_direct_min(ncrc > 0)) return false;
-  constexpr uintptr_t kPage = 4096;
-  constexpr size_t kMinMid = 32u << 10;
-  // the rows the call touches: live inputs, then outputs
-  std::vector<uintptr_t> rows;
-  for (int i = 0; i < nin; ++i)
-    if (din[i]) rows.push_back(reinterpret_cast<uintptr_t>(din[i]));
-  for (int o = 0; o < nout; ++o) rows.push_back(reinterpret_cast<uintptr_t>(out_rows[o]));
-  size_t c0 = 0, tmax = 0;
-  for (uintptr_t a : rows) {
-    if (a & 15) return false;  // the vector kernels need 16-byte rows
-    c0 = std::max<size_t>(c0, (kPage - (a & (kPage - 1))) & (kPage - 1));
-    tmax = std::max<size_t>(tmax, (a + len) & (kPage - 1));
-  }
-  if (len < c0 + tmax + kMinMid) return false;
-  const size_t mid = (len - c0 - tmax) / hrs::kWindowBytes * hrs::kWindowBytes;
-  const size_t c1 = c0 + mid, tlen = len - c1;
-  if (mid < kMinMid) return false;
-  if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, mid, 1)) return false;
-  if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, mid)) return false;
-  // registration ranges: the whole pages of each row under [c0, c1)
-  std::vector<std::pair<uintptr_t, uintptr_t>> rg;
-  for (uintptr_t a : rows) rg.push_back({(a + c0) & ~(kPage - 1), (a + c1 + kPage - 1) & ~(kPage - 1)});
-  // staging for the head and tail columns (pinned, device-mapped), their CRC
-  // words, and the raw window-CRC scratch: all before any page is registered.
-  // The head and the tail run as ONE launch of two "stripes" (stripe 0 the
-  // head, 1 the tail) of W-byte staging rows, each segment right-aligned
-  // behind a zero pad: columns are independent, a raw CRC ignores leading
-  // zeros, and W is a whole number of 2 KiB windows, so a checksummed call's
-  // head / tail take the fused kernel too (the pad's length term in the CRC is
-  // taken out on the host, pad_fix).
-  const int nrows = nlive + nout;
-  const size_t W = (c0 || tlen) ? (std::max(c0, tlen) + hrs::kWindowBytes - 1) / hrs::kWindowBytes * hrs::kWindowBytes
-                                : 0;
-  const size_t ht_stride = W * nrows;  // head stripe, then tail stripe
-  const size_t crc_off = 2 * ht_stride;
-  const size_t need = crc_off + 3 * static_cast<size_t>(std::max(ncrc, 1)) * sizeof(uint32_t);
-  hrs_status s0 = host_slot(c, 0, need);
-  if (s0 == HRS_OK && !c->host[0].pin_dev) return false;  // staging not device-mapped at its own address
-  // raw window-CRC scratch: the middle's, then the head / tail's (they run
-  // at the same time on two streams)
-  const size_t raw_mid = ncrc > 0 ? (crc_raw_bytes_for(mid, 1, ncrc) + 255) & ~static_cast<size_t>(255) : 0;
-  const size_t raw_need = ncrc > 0 ? raw_mid + crc_raw_bytes_for(std::max<size_t>(W, 1), 2, ncrc) : 0;
-  if (s0 == HRS_OK && W) s0 = host_slot(c, 1, 0);  // the head / tail stream
-  if (s0 == HRS_OK && raw_need > c->direct_raw_bytes) {
-    if (c->direct_raw) (void)hipFree(c->direct_raw);  // no call of this handle is in flight
-    c->direct_raw = nullptr;
-    c->direct_raw_bytes = 0;
-    hipError_t e = hipMalloc(&c->direct_raw, raw_need);
-    if (e != hipSuccess) s0 = fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", raw_need, hipGetErrorString(e));
-    else c->direct_raw_bytes = raw_need;
-  }
-  if (s0 != HRS_OK) {
-    *st = s0;
-    return true;
-  }
-  DirectTurn turn(c->device);
-  if (!turn.ok) return false;
-  RegisteredPages reg(std::move(rg));  // merged: a row passed twice, or rows back to back, register once
-  if (!reg.ok()) return false;
-  hrs_codec::HostSlot& h = c->host[0];
-  const hipStream_t s = h.stream, s_ht = c->host[1].stream;
-  c->last_host_path = "direct";
-  // row pointers: the middle's in the caller's memory; the head / tail's in
-  // the staging (live inputs first, then outputs, as `rows`), row j of
-  // stripe t at t * ht_stride + j * W, its segment in the last bytes
-  std::vector<const uint8_t*> in_ht(nin, nullptr), in_m(nin, nullptr);
-  std::vector<uint8_t*> out_ht(nout), out_m(nout);
-  {
-    int j = 0;
-    for (int i = 0; i < nin; ++i) {
-      if (!din[i]) continue;
-      in_m[i] = din[i] + c0;
-      if (W) in_ht[i] = h.pin_dev + W * j;
-      ++j;
-    }
-    for (int o = 0; o < nout; ++o, ++j) {
-      out_m[o] = out_rows[o] + c0;
-      out_ht[o] = h.pin_dev + W * j;
-    }
-  }
-  uint32_t* crc_dev = reinterpret_cast<uint32_t*>(h.pin_dev + crc_off);  // head, tail, middle: ncrc words each
-  auto segment = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, size_t stride,
-                     size_t sl, size_t nst, uint32_t* cw, hipStream_t ss, uint32_t* raw) -> hrs_status {
-    if (crc.mode == kCrcEncode)
-      return encode_crc_impl(c, in.data(), stride, out.data(), stride, sl, nst, nullptr, cw, ss, raw);
-    if (crc.mode == kCrcOutputs)
-      return apply_crc_impl(c, m, nout, nin, in.data(), stride, out.data(), stride, sl, nst, nullptr, cw, ss, raw);
-    return run_apply(c, m, nout, nin, in.data(), stride, out.data(), stride, sl, nst, ss, static_kp);
-  };
-  // the middle is launched first, on slot 0's stream; the head / tail
-  // columns are copied into the staging while it runs and launched on slot
-  // 1's stream, beside it instead of after it
-  uint32_t* raw_ht = c->direct_raw ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(c->direct_raw) + raw_mid)
-                                   : nullptr;
-  hrs_status rs = HRS_OK;
-  {
-    hrs::GridCap cap(zero_copy_blocks());
-    rs = segment(in_m, out_m, 0, mid, 1, crc_dev + 2 * ncrc, s, c->direct_raw);
-    if (rs == HRS_OK && W) {
-      int j = 0;
-      for (int i = 0; i < nin; ++i) {
-        if (!din[i]) continue;
-        uint8_t* hr = h.pin + W * j++;
-        uint8_t* tr = hr + ht_stride;
-        if (ncrc > 0) {  // the CRC reads the pads: zeros
-          std::memset(hr, 0, W - c0);
-          std::memset(tr, 0, W - tlen);
-        }
-        std::memcpy(hr + (W - c0), din[i], c0);
-        std::memcpy(tr + (W - tlen), din[i] + c1, tlen);
-      }
-      rs = segment(in_ht, out_ht, ht_stride, W, 2, crc_dev, s_ht, raw_ht);
-    }
-  }
-  // whatever the launches did, nothing may touch the pages once they are unregistered
-  hipError_t e = hipStreamSynchronize(s);
-  if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
-  if (W) {
-    e = hipStreamSynchronize(s_ht);
-    if (rs == HRS_OK && e != hipSuccess) rs = hip_fail(c, e, "hipStreamSynchronize");
-  }
-  reg.release();
-  if (rs == HRS_OK) {
-    for (int o = 0; o < nout; ++o) {
-      const uint8_t* hr = h.pin + W * (nlive + o);
-      std::memcpy(out_rows[o], hr + (W - c0), c0);
-      std::memcpy(out_rows[o] + c1, hr + ht_stride + (W - tlen), tlen);
-    }
-    // CRC32.update chaining over the three column segments in order. A
-    // padded segment's fold returned crc32(0, pad || D) = crc32(0, D) ^
-    // Z_W(~0) ^ Z_|D|(~0) (crc32.hpp: the raw part ignores leading zeros)
-    const uint32_t* part = reinterpret_cast<const uint32_t*>(h.pin + crc_off);
-    auto pad_fix = [&](size_t d) {
-      return hrs::crc::apply(crc_zmat(c, W), ~0u) ^ hrs::crc::apply(crc_zmat(c, d), ~0u);
-    };
-    const size_t seg_len[3] = {c0, mid, tlen};
-    const int seg_word[3] = {0, 2, 1};
-    for (int seg = 0; seg < 3 && ncrc > 0; ++seg) {
-      if (!seg_len[seg]) continue;
-      const hrs::crc::Mat& z = crc_zmat(c, seg_len[seg]);
-      const uint32_t fix = seg == 1 ? 0u : pad_fix(seg_len[seg]);
-      for (int r = 0; r < ncrc; ++r)
-        crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[seg_word[seg] * ncrc + r] ^ fix;
-    }
-  }
-  *st = rs;
-  return true;
-}
-
-// Rows the caller already holds in pinned memory (hipHostMalloc'd, or
-// registered by the caller) are visible to the GPU at their own addresses and
-// never move: the zero-copy kernel runs over them in place, one launch, no
-// staging copies and no registrations ("pinned"). Taken when zero copy is on,
-// every live input and output row is pinned and 16-byte aligned, and a
+// Rows the caller holds in memory the runtime allocated pinned (hipHostMalloc,
+// torch pin_memory) are visible to the GPU at their own addresses and never
+// move: the zero-copy kernel runs over them in place, one launch, no staging
+// copies ("pinned"). Taken when zero copy is on, every live input and output
+// row lies wholly inside such an allocation and is 16-byte aligned, and a
 // checksummed call's kernel is one-pass (a two-pass CRC would read the cells
 // across the link twice); otherwise false and nothing done.
+// Pageable memory the caller registered with hipHostRegister is NOT taken
+// here: registration maps the pages for the GPU without pinning them, and in
+// round 5 GPU writes into registered pages were lost when a page moved during
+// a kernel ("Platform constraint"). Such rows are staged.
 bool host_apply_pinned(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* din,
                        uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc,
                        hrs_status* st) {
@@ -393,12 +115,12 @@ bool host_apply_pinned(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
   for (int i = 0; i < nin; ++i) {
     if (!din[i]) continue;
     uint8_t* d = nullptr;
-    if (!aligned16(din[i]) || !host_device_ptr(din[i], &d) || d != din[i]) return false;
+    if (!aligned16(din[i]) || !host_device_ptr(din[i], len, &d) || d != din[i]) return false;
     ++nlive;
   }
   for (int o = 0; o < nout; ++o) {
     uint8_t* d = nullptr;
-    if (!aligned16(out_rows[o]) || !host_device_ptr(out_rows[o], &d) || d != out_rows[o]) return false;
+    if (!aligned16(out_rows[o]) || !host_device_ptr(out_rows[o], len, &d) || d != out_rows[o]) return false;
   }
   if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, len, 1)) return false;
   if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, len)) return false;
@@ -461,7 +183,6 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     for (int i = 0; i < nin; ++i) live_rows[i] = slot_of[i] >= 0 ? in_rows[i] : nullptr;
     hrs_status st = HRS_OK;
     if (host_apply_pinned(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, &st)) return st;
-    if (host_apply_direct(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, nlive, &st)) return st;
   }
   const size_t chunk = std::min(len, host_chunk_bytes());
   const size_t pitch = pitch_for(chunk);
@@ -605,7 +326,7 @@ hrs_status async_slot(hrs_codec* c, hrs_codec::AsyncSlot& a, size_t bytes) {
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   e = hipHostMalloc(&a.pin, bytes, hipHostMallocDefault);
   if (e != hipSuccess) return fail(c, HRS_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
-  if (!host_device_ptr(a.pin, &a.pin_dev)) a.pin_dev = nullptr;
+  if (!host_device_ptr(a.pin, bytes, &a.pin_dev)) a.pin_dev = nullptr;
   a.bytes = bytes;
   return HRS_OK;
 }

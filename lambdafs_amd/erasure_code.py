@@ -258,7 +258,8 @@ class _HipErasureCode(ErasureCode):
 
     def lastHostPath(self):
         """How the latest synchronous host-buffer call moved its bytes
-        (hrs_last_host_path): "pinned", "staged", "direct" (opt-in), "copy_engine" or ""."""
+        (hrs_last_host_path): "pinned" (runtime-pinned rows, zero copy in place),
+        "staged", "copy_engine" or ""."""
         return _lib.lib().hrs_last_host_path(self._handle()).decode()
 
     def encodeMatrix(self):

@@ -34,18 +34,6 @@ def test_host_logic_vs_oracle():
     assert out.returncode == 0 and res["ok"], res
 
 
-def test_page_claims_concurrent_holders():
-    """The process-wide claims on the host pages the synchronous direct calls
-    register (hrs_host.hpp PageClaims): overlap rules, and 8 threads claiming
-    random ranges at once never hold one page twice."""
-    exe = os.path.join(ROOT, "tests", "cpp", "page_claims_test")
-    if not os.path.exists(exe):
-        subprocess.check_call(["make", "-C", ROOT, "tests/cpp/page_claims_test"])
-    out = subprocess.run([exe, "8", "20000"], capture_output=True, text=True, timeout=120)
-    res = json.loads(out.stdout.strip().splitlines()[-1])
-    assert out.returncode == 0 and res["ok"] and res["granted"] > 0 and res["refused"] > 0, res
-
-
 @pytest.mark.parametrize("threads", [0, 1, 4, 8])
 def test_copy_pool_concurrent_callers(threads):
     """The host copy pool (hrs_host.hpp) under 4 concurrent callers posting

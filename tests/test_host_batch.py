@@ -31,7 +31,6 @@ def transfer_mode(request, monkeypatch):
     (HRS_HBATCH_DUPLEX=1: in_done / comp_done / done events chain the three
     streams per slot)."""
     monkeypatch.delenv("HRS_HBATCH_DUPLEX", raising=False)
-    monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
     if request.param == "zero_copy":
         monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
     else:
@@ -225,7 +224,7 @@ def test_host_batches_on_interior_pinned_views(cuda):
 def test_pageable_batches_path_and_parity(cuda, transfer_mode, offset):
     """Pageable batches that start `offset` bytes past a page boundary (0: the
     stripes fill whole pages; otherwise the first and last stripes reach into
-    partial pages and are staged after the registered middle). The path each
+    partial pages: every pageable batch is staged whole). The path each
     mode takes (hrs_last_host_path), parity vs the oracle for every stripe,
     and every repaired cell; pinned buffers report "pinned"."""
     torch = cuda
@@ -264,8 +263,7 @@ def test_pageable_batches_path_and_parity(cuda, transfer_mode, offset):
 def test_pageable_multi_batch(cuda, transfer_mode):
     """hrs_decode_batch_host_multi over the device set {0, 0} on pageable
     memory starting 48 bytes past a page boundary: every repaired cell and
-    every parity row checked (test_host_direct.py runs the same with the
-    opt-in direct path)."""
+    every parity row checked."""
     k, p, S, L = 12, 4, 16, 64 << 10
     n = k + p
     codes = [HipReedSolomonCode(k, p, device=0) for _ in range(2)]

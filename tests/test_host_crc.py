@@ -29,17 +29,10 @@ def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
     bytes: the staged zero-copy path (the default: rows copied into pinned
     staging, the kernel works on the staging across the link) and the copy
-    engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H). The opt-in
-    direct path (HRS_HOST_DIRECT=1) has its own suite, test_host_direct.py,
-    kept small: registered pageable pages are not pinned, and a page moved
-    during a call loses the GPU's writes to it (profiles/r05/NOTES.md), so
-    every direct call in the default run is a small chance of a spurious
-    failure."""
-    monkeypatch.delenv("HRS_HOST_DIRECT", raising=False)
+    engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H). Which caller memory runs in place
+    (runtime-pinned only) is test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
-    if request.param == "direct":
-        monkeypatch.setenv("HRS_HOST_DIRECT", "1")
-    elif request.param == "copy_engine":
+    if request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
     return request.param
 

@@ -1,5 +1,5 @@
 """Long runs of the seeded differential fuzz suites (tests/test_gpu_fuzz.py,
-tests/test_host_direct.py::test_direct_fuzz) with other seeds and more cases
+tests/test_host_memory.py::test_host_call_fuzz) with other seeds and more cases
 than the default `-m gpu` run affords: a bug hunt, not a test. Each seed is
 one call of the suite's own test function, so a failure names its case.
 Usage: python tests/tools/fuzz_long.py [seeds] [cases] (one JSON line per seed)"""
@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
 
 import test_gpu_fuzz as F  # noqa: E402
-import test_host_direct as D  # noqa: E402
+import test_host_memory as D  # noqa: E402
 
 
 def main():
@@ -40,11 +40,11 @@ def main():
         F.test_differential_fuzz(torch)
         print(json.dumps({"suite": "test_gpu_fuzz", "seed": F.SEED, "cases": cases, "ok": True,
                           "s": round(time.time() - t0, 1)}), flush=True)
-        D.DIRECT_FUZZ_SEED, D.DIRECT_FUZZ_CASES = 0xD1EC7 + 104729 * (i + 1), max(40, cases // 10)
+        D.FUZZ_SEED, D.FUZZ_CASES = 0xD1EC7 + 104729 * (i + 1), max(40, cases // 10)
         t0 = time.time()
-        D.test_direct_fuzz(torch)
-        print(json.dumps({"suite": "test_host_direct.test_direct_fuzz", "seed": D.DIRECT_FUZZ_SEED,
-                          "cases": D.DIRECT_FUZZ_CASES, "ok": True, "s": round(time.time() - t0, 1)}), flush=True)
+        D.test_host_call_fuzz(torch)
+        print(json.dumps({"suite": "test_host_memory.test_host_call_fuzz", "seed": D.FUZZ_SEED,
+                          "cases": D.FUZZ_CASES, "ok": True, "s": round(time.time() - t0, 1)}), flush=True)
 
 
 if __name__ == "__main__":
