@@ -22,12 +22,16 @@ JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
             tests/cpp/copy_pool_test
 
-TOOLS    := tools/host_call_rate
+TOOLS    := tools/host_call_rate tools/host_pipeline_sweep
 
 all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
 
 # The synchronous C-ABI call rate (bench.py's host_calls leg, profiles/r05/).
 tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
+
+# A/B of the staged pipeline's knobs, interleaved in one process (profiles/r06/).
+tools/host_pipeline_sweep: tools/host_pipeline_sweep.cpp include/hrs.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
@@ -61,11 +65,16 @@ build/hrs_decode_crc.o: lambdafs_amd/csrc/hrs_decode_crc.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+build/hrs_gate.o: lambdafs_amd/csrc/hrs_gate.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 build/hrs_probe.o: lambdafs_amd/csrc/hrs_probe.hip include/hrs_probe.h $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_decode_crc.o
+KOBJ     := build/hrs_kernels.o build/hrs_runtime.o build/hrs_batch.o build/hrs_crc.o build/hrs_fused.o build/hrs_decode_crc.o \
+            build/hrs_gate.o
 
 $(LIB): $(API_OBJ) $(KOBJ) lambdafs_amd/csrc/libhrs.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=lambdafs_amd/csrc/libhrs.map -o $@ $(API_OBJ) $(KOBJ) \

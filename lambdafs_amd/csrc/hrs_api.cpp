@@ -195,6 +195,7 @@ void hrs_destroy(hrs_codec* c) {
     if (h.dev) (void)hipFree(h.dev);
     if (h.pin) (void)hipHostFree(h.pin);
   }
+  if (c->qflags) (void)hipHostFree(c->qflags);  // every slot stream has drained above
   for (auto& a : c->async) {
     if (a.stream) {
       (void)hipStreamSynchronize(a.stream);

@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -73,6 +74,13 @@ struct hrs_codec {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
   } host[hrs::kHostSlots];
+  // gated staged pipeline (hrs_hostpath.cpp staged_run): coherent pinned
+  // ready / done / miss words, the next chunk tag, the gates' timeout in
+  // wall-clock ticks, and the chunk shapes (CRC mode, length) run before
+  uint32_t* qflags = nullptr;
+  uint32_t qtag = 0;
+  uint64_t gate_timeout = 0;
+  std::set<uint64_t> staged_shapes;
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
   // its own compute stream; every slot's H2D goes on one copy-in stream and

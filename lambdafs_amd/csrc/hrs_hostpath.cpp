@@ -6,10 +6,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hrs.h"
@@ -23,33 +26,6 @@ namespace hrs::api {
 
 // Device scratch for the host-buffer calls: `rows` rows of `pitch` bytes.
 size_t pitch_for(size_t len) { return (len + 255) & ~static_cast<size_t>(255); }
-
-// Host rows -> device, apply m, device -> host rows; synchronous. The rows
-// (pageable: a JNI-pinned Java array) go through pinned staging in column
-// chunks over a ring of slots (2 by default): while the copy pool moves chunk
-// j into one slot's staging (and chunk j - nslots's outputs out of it), the GPU
-// runs the previous chunks' H2D, kernel and D2H on the other slots' streams.
-size_t host_chunk_bytes() {
-  static const size_t v = [] {
-    const char* e = getenv("HRS_HOST_CHUNK");
-    long x = e ? atol(e) : 0;
-    if (x < static_cast<long>(hrs::kWindowBytes)) x = 512 << 10;  // measured best (tools/host_sweep.sh)
-    return static_cast<size_t>(x) / hrs::kWindowBytes * hrs::kWindowBytes;
-  }();
-  return v;
-}
-
-// Chunk slots a call rotates through: 2 (the default) or up to kHostSlots,
-// so the copy of chunk j need not wait for chunk j - 2's kernel (HRS_HOST_SLOTS,
-// read once).
-int host_slots() {
-  static const int v = [] {
-    const char* e = getenv("HRS_HOST_SLOTS");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 2 && x <= hrs::kHostSlots) ? x : 2;
-  }();
-  return v;
-}
 
 hrs_status host_slot(hrs_codec* c, int i, size_t bytes) {
   hrs_codec::HostSlot& h = c->host[i];
@@ -158,6 +134,269 @@ bool host_apply_pinned(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
   return true;
 }
 
+// ---- the staged pipeline (pageable rows) ----
+// The caller's rows are cut into column chunks (the first HRS_HOST_FIRST
+// bytes, then HRS_HOST_CHUNK each) that rotate through a ring of S slots
+// (HRS_HOST_SLOTS), each with its own pinned staging and stream. Per chunk:
+// the copy pool moves its live input columns into the slot's staging, the
+// zero-copy kernel works on the staging across the link (or, HRS_ZEROCOPY=0
+// and for chunks no one-pass kernel takes, H2D -> kernel -> D2H), and the
+// pool moves its output columns out. Chunks are copied out in order as soon
+// as they are done (not only when their slot is needed again), so only the
+// last chunk's copy-out follows the link time; each chunk's CRC words are
+// kept and chained in order at the end.
+// Gated (HRS_HOST_GATE=1): every chunk's kernels are queued S chunks ahead,
+// each behind a gate kernel that waits for the chunk's tag in a pinned flag
+// word (hrs_gate.hip) and followed by a signal kernel the host polls; the host
+// publishes the tag as soon as the copy-in ends, so no launch sits between a
+// chunk's copy-in and its kernel. Without gates a chunk is launched after its
+// copy-in and its completion is an event.
+static size_t env_window_bytes(const char* name, size_t dflt) {
+  const char* e = getenv(name);
+  const long x = e ? atol(e) : 0;
+  if (x < static_cast<long>(hrs::kWindowBytes)) return dflt;
+  return static_cast<size_t>(x) / hrs::kWindowBytes * hrs::kWindowBytes;
+}
+
+size_t host_chunk_bytes() { return env_window_bytes("HRS_HOST_CHUNK", 512 << 10); }
+size_t host_first_bytes(size_t chunk) { return std::min(chunk, env_window_bytes("HRS_HOST_FIRST", chunk)); }
+
+int host_slots() {
+  const char* e = getenv("HRS_HOST_SLOTS");
+  const int x = e ? atoi(e) : 0;
+  return (x >= 2 && x <= hrs::kHostSlots) ? x : 2;
+}
+
+bool host_gate_on() {
+  const char* e = getenv("HRS_HOST_GATE");
+  return e && e[0] == '1';
+}
+
+// Coherent pinned flag words of the gated pipeline, one 128-byte line each:
+// ready[kHostSlots], done[kHostSlots], then the gates' miss word.
+constexpr int kFlagWords = 32;
+inline uint32_t* flag_ready(hrs_codec* c, int sl) { return c->qflags + sl * kFlagWords; }
+inline uint32_t* flag_done(hrs_codec* c, int sl) { return c->qflags + (hrs::kHostSlots + sl) * kFlagWords; }
+inline uint32_t* flag_fail(hrs_codec* c) { return c->qflags + 2 * hrs::kHostSlots * kFlagWords; }
+
+bool gate_flags(hrs_codec* c) {
+  if (c->qflags) return true;
+  void* p = nullptr;
+  const size_t bytes = (2 * hrs::kHostSlots + 1) * kFlagWords * sizeof(uint32_t);
+  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  uint8_t* d = nullptr;
+  if (!host_device_ptr(p, bytes, &d)) {  // the gates read the flags at their host address
+    (void)hipHostFree(p);
+    return false;
+  }
+  std::memset(p, 0, bytes);
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
+  c->gate_timeout = static_cast<uint64_t>(khz) * 1000u * 10u;  // 10 s of wall-clock ticks
+  c->qflags = static_cast<uint32_t*>(p);
+  return true;
+}
+
+inline uint32_t flag_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline bool tag_reached(uint32_t v, uint32_t want) { return static_cast<int32_t>(v - want) >= 0; }
+
+hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
+                      uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc,
+                      const std::vector<int>& slot_of, int nlive, bool gate, bool* missed) {
+  *missed = false;
+  struct Span {
+    size_t off, len;
+  };
+  const size_t chunk = std::min(len, host_chunk_bytes());
+  const size_t first = host_first_bytes(chunk);
+  std::vector<Span> ch;
+  for (size_t off = 0; off < len;) {
+    const size_t l = std::min(ch.empty() ? first : chunk, len - off);
+    ch.push_back({off, l});
+    off += l;
+  }
+  const size_t C = ch.size();
+  const int S = static_cast<int>(std::min<size_t>(host_slots(), C));
+  const size_t pitch = pitch_for(chunk);
+  // slot layout: nlive + nout rows of `pitch`, then (CRC only) the chunk's
+  // ncrc CRC words, then the raw window-CRC scratch (device side only)
+  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
+  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
+  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(chunk, 1, ncrc) : crc_off;
+  for (int i = 0; i < S; ++i) {
+    hrs_status st = host_slot(c, i, need);
+    if (st != HRS_OK) return st;
+  }
+  // zero copy: the kernel reads the chunk from the slot's pinned staging and
+  // writes its outputs (and the chunk CRCs) there, across the host link — no
+  // H2D / D2H. A checksummed chunk goes this way only when its one-pass
+  // kernel takes it (a two-pass CRC would read the cells across the link a
+  // second time); other chunks take the copy engine. The raw window CRCs stay
+  // in device memory.
+  bool zc_ok = zero_copy_on();
+  for (int i = 0; i < S; ++i) zc_ok &= c->host[i].pin_dev != nullptr;
+  auto zc_chunk = [&](size_t lj) {
+    if (!zc_ok) return false;
+    if (crc.mode == kCrcEncode) return encode_crc_one_pass(c, lj, 1);
+    if (crc.mode == kCrcOutputs) return apply_crc_one_pass(c, nout, nlive, lj);
+    return true;
+  };
+  // Gates only for chunk shapes this handle has run before: a first run may
+  // upload CRC tables (a synchronous copy, and an LRU eviction's hipFree
+  // waits for the device) while its own gates hold the slot streams.
+  auto shape = [&](size_t lj) { return static_cast<uint64_t>(crc.mode) << 56 | static_cast<uint64_t>(lj); };
+  bool all_zc = true, seen = true;
+  for (const Span& sp : ch) {
+    all_zc &= zc_chunk(sp.len);
+    seen &= c->staged_shapes.count(shape(sp.len)) > 0;
+  }
+  gate = gate && all_zc && seen && gate_flags(c);
+  c->last_host_path = all_zc ? "staged" : "copy_engine";
+  hrs::CopyPool& pool = hrs::CopyPool::instance();
+  std::vector<hrs::CopyJob> jobs;
+  std::vector<uint32_t> parts(static_cast<size_t>(ncrc) * C);
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  auto copy_in = [&](size_t j) {
+    const hrs_codec::HostSlot& h = c->host[j % S];
+    jobs.clear();
+    for (int i = 0; i < nin; ++i)
+      if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + ch[j].off, ch[j].len});
+    pool.run(jobs);
+  };
+  auto copy_out = [&](size_t j) {
+    const hrs_codec::HostSlot& h = c->host[j % S];
+    jobs.clear();
+    for (int o = 0; o < nout; ++o) jobs.push_back({out_rows[o] + ch[j].off, h.pin + pitch * (nlive + o), ch[j].len});
+    pool.run(jobs);
+    if (ncrc) std::memcpy(&parts[j * ncrc], h.pin + crc_off, ncrc * sizeof(uint32_t));
+  };
+  // the chunk's kernels (and, off the zero-copy path, its H2D and D2H) on its slot's stream
+  auto launch = [&](size_t j) -> hrs_status {
+    hrs_codec::HostSlot& h = c->host[j % S];
+    const size_t lj = ch[j].len;
+    const bool zc = zc_chunk(lj);
+    // only zero-copy chunks cap their grid (the link bounds them); a chunk
+    // sent back to the copy engine runs on device memory with the full grid
+    hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
+    if (nlive > 0 && !zc) {
+      hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
+    }
+    uint8_t* img = zc ? h.pin_dev : h.dev;
+    for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
+    for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
+    uint32_t* dcrc = reinterpret_cast<uint32_t*>(img + crc_off);
+    uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
+    hrs_status st;
+    if (crc.mode == kCrcEncode)
+      st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+    else if (crc.mode == kCrcOutputs)  // repair + CRC of the repaired cells (fused where the shape allows)
+      st = apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+    else
+      st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
+    if (st != HRS_OK) return st;
+    if (!zc) {  // outputs (and the chunk CRCs right behind them) back to the staging
+      const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + lj;
+      hipError_t e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost,
+                                    h.stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
+    }
+    return HRS_OK;
+  };
+  size_t out_next = 0;  // chunks [0, out_next) are copied out
+  hrs_status st = HRS_OK;
+  if (gate) {
+    const uint32_t tag0 = c->qtag;
+    c->qtag += static_cast<uint32_t>(C);
+    auto tag = [&](size_t j) { return tag0 + static_cast<uint32_t>(j) + 1u; };
+    // test hooks (tests/test_host_path.py): a short gate timeout and a host
+    // stall before chunk 1 is published exercise the miss -> re-run path
+    const char* te = getenv("HRS_GATE_TIMEOUT_US");
+    const uint64_t timeout = te && atol(te) > 0 ? c->gate_timeout / 10000000u * static_cast<uint64_t>(atol(te))
+                                                : c->gate_timeout;
+    const char* de = getenv("HRS_GATE_DELAY_US");
+    const long delay_us = de ? atol(de) : 0;
+    auto enqueue = [&](size_t j) -> hrs_status {
+      const int sl = static_cast<int>(j % S);
+      const hipStream_t hs = c->host[sl].stream;
+      hipError_t e = hrs::launch_gate(flag_ready(c, sl), tag(j), flag_fail(c), timeout, hs);
+      if (e != hipSuccess) return hip_fail(c, e, "gate launch");
+      hrs_status s2 = launch(j);
+      if (s2 != HRS_OK) return s2;
+      e = hrs::launch_signal(flag_done(c, sl), tag(j), hs);
+      return e == hipSuccess ? HRS_OK : hip_fail(c, e, "signal launch");
+    };
+    auto done = [&](size_t j) { return tag_reached(flag_load(flag_done(c, static_cast<int>(j % S))), tag(j)); };
+    auto wait_done = [&](size_t j) -> hrs_status {
+      for (uint32_t spin = 1; !done(j); ++spin) {
+        if ((spin & 4095u) == 0) {  // a failed stream never signals: surface its error
+          const hipError_t e = hipStreamQuery(c->host[j % S].stream);
+          if (e != hipSuccess && e != hipErrorNotReady) return hip_fail(c, e, "staged chunk");
+        }
+        __builtin_ia32_pause();
+      }
+      return HRS_OK;
+    };
+    for (size_t j = 0; j < static_cast<size_t>(S) && st == HRS_OK; ++j) st = enqueue(j);
+    for (size_t j = 0; j < C && st == HRS_OK; ++j) {
+      while (st == HRS_OK && out_next + S <= j) {  // the slot's previous chunk must be out
+        st = wait_done(out_next);
+        if (st == HRS_OK) copy_out(out_next++);
+      }
+      if (st != HRS_OK) break;
+      copy_in(j);
+      if (j == 1 && delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+      __atomic_store_n(flag_ready(c, static_cast<int>(j % S)), tag(j), __ATOMIC_RELEASE);
+      if (j + S < C) st = enqueue(j + S);
+      while (st == HRS_OK && out_next < j && done(out_next)) copy_out(out_next++);
+    }
+    while (st == HRS_OK && out_next < C) {
+      st = wait_done(out_next);
+      if (st == HRS_OK) copy_out(out_next++);
+    }
+    if (st != HRS_OK) {  // open every gate of this call so its queued work drains
+      for (int sl = 0; sl < S; ++sl) __atomic_store_n(flag_ready(c, sl), tag0 + static_cast<uint32_t>(C), __ATOMIC_RELEASE);
+      return st;
+    }
+    if (__atomic_load_n(flag_fail(c), __ATOMIC_ACQUIRE)) {
+      __atomic_store_n(flag_fail(c), 0u, __ATOMIC_RELEASE);
+      *missed = true;
+      return HRS_OK;
+    }
+  } else {
+    auto ev = [&](size_t j) { return c->host[j % S].done; };
+    for (size_t j = 0; j < C; ++j) {
+      while (out_next + S <= j) {
+        hipError_t e = hipEventSynchronize(ev(out_next));
+        if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
+        copy_out(out_next++);
+      }
+      copy_in(j);
+      st = launch(j);
+      if (st != HRS_OK) return st;
+      hipError_t e = hipEventRecord(ev(j), c->host[j % S].stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+      while (out_next < j && hipEventQuery(ev(out_next)) == hipSuccess) copy_out(out_next++);
+    }
+    while (out_next < C) {
+      hipError_t e = hipEventSynchronize(ev(out_next));
+      if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
+      copy_out(out_next++);
+    }
+  }
+  if (c->staged_shapes.size() > 256) c->staged_shapes.clear();
+  for (const Span& sp : ch) c->staged_shapes.insert(shape(sp.len));
+  for (size_t j = 0; j < C && ncrc; ++j) {  // CRC32.update chaining over the chunks in column order
+    const hrs::crc::Mat& z = crc_zmat(c, ch[j].len);
+    for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ parts[j * ncrc + r];
+  }
+  return HRS_OK;
+}
+
 hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                            uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc) {
   const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
@@ -184,105 +423,15 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     hrs_status st = HRS_OK;
     if (host_apply_pinned(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, &st)) return st;
   }
-  const size_t chunk = std::min(len, host_chunk_bytes());
-  const size_t pitch = pitch_for(chunk);
-  const size_t nchunks = (len + chunk - 1) / chunk;
-  // slot layout: nlive + nout rows of `pitch`, then (CRC only) the chunk's
-  // ncrc CRC words, then the raw window-CRC scratch (device side only)
-  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
-  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
-  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(chunk, 1, ncrc) : crc_off;
-  const int nslots = host_slots();
-  for (int i = 0; i < nslots; ++i) {
-    hrs_status st = host_slot(c, i, need);
-    if (st != HRS_OK) return st;
+  std::vector<uint32_t> start(crc.out, crc.out + ncrc);  // crc.out may alias crc.in: kept for a re-run
+  bool missed = false;
+  hrs_status st = staged_run(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc, ncrc, slot_of, nlive,
+                             host_gate_on(), &missed);
+  if (st == HRS_OK && missed) {  // a gate gave up waiting: discard everything and run it without gates
+    std::copy(start.begin(), start.end(), crc.out);
+    st = staged_run(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc, ncrc, slot_of, nlive, false, &missed);
   }
-  // zero copy: the kernel reads the chunk from the slot's pinned staging and
-  // writes its outputs (and the chunk CRCs) there, across the host link — no
-  // H2D / D2H. A checksummed chunk goes this way only when its one-pass
-  // kernel takes it (a two-pass CRC would read the cells across the link a
-  // second time); other chunks take the copy engine. The raw window CRCs stay
-  // in device memory.
-  uint8_t* zpin[hrs::kHostSlots] = {};
-  bool zc_ok = zero_copy_on();
-  for (int i = 0; i < nslots; ++i) zc_ok &= (zpin[i] = c->host[i].pin_dev) != nullptr;
-  auto zc_chunk = [&](size_t lj) {
-    if (!zc_ok) return false;
-    if (crc.mode == kCrcEncode) return encode_crc_one_pass(c, lj, 1);
-    if (crc.mode == kCrcOutputs) return apply_crc_one_pass(c, nout, nlive, lj);
-    return true;
-  };
-  hrs::CopyPool& pool = hrs::CopyPool::instance();
-  std::vector<hrs::CopyJob> jobs;
-  size_t pend_off[hrs::kHostSlots] = {}, pend_len[hrs::kHostSlots] = {};
-  bool pending[hrs::kHostSlots] = {};
-  auto finish = [&](int sl) -> hrs_status {  // wait for a slot, copy its outputs out
-    if (!pending[sl]) return HRS_OK;
-    hipError_t e = hipEventSynchronize(c->host[sl].done);
-    if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
-    jobs.clear();
-    for (int o = 0; o < nout; ++o)
-      jobs.push_back({out_rows[o] + pend_off[sl], c->host[sl].pin + pitch * (nlive + o), pend_len[sl]});
-    pool.run(jobs);
-    if (ncrc) {  // chunks finish in order: chain this one onto the running values
-      const uint32_t* part = reinterpret_cast<const uint32_t*>(c->host[sl].pin + crc_off);
-      const hrs::crc::Mat& z = crc_zmat(c, pend_len[sl]);
-      for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[r];
-    }
-    pending[sl] = false;
-    return HRS_OK;
-  };
-  std::vector<const uint8_t*> din(nin);
-  std::vector<uint8_t*> dout(nout);
-  for (size_t j = 0; j < nchunks; ++j) {
-    const int sl = static_cast<int>(j % nslots);
-    hrs_codec::HostSlot& h = c->host[sl];
-    hrs_status st = finish(sl);
-    if (st != HRS_OK) return st;
-    const size_t off = j * chunk, lj = std::min(chunk, len - off);
-    jobs.clear();
-    for (int i = 0; i < nin; ++i)
-      if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + off, lj});
-    pool.run(jobs);
-    const bool zc = zc_chunk(lj);
-    c->last_host_path = zc ? "staged" : "copy_engine";
-    // only zero-copy chunks cap their grid (the link bounds them); a chunk
-    // sent back to the copy engine runs on device memory with the full grid
-    hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
-    if (nlive > 0 && !zc) {
-      hipError_t e = hipMemcpyAsync(h.dev, h.pin, pitch * (nlive - 1) + lj, hipMemcpyHostToDevice, h.stream);
-      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync H2D");
-    }
-    uint8_t* img = zc ? zpin[sl] : h.dev;
-    for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
-    for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
-    uint32_t* dcrc = reinterpret_cast<uint32_t*>(img + crc_off);
-    uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
-    if (crc.mode == kCrcEncode)
-      st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
-    else if (crc.mode == kCrcOutputs)  // repair + CRC of the repaired cells (fused where the shape allows)
-      st = apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
-    else
-      st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
-    if (st != HRS_OK) return st;
-    // outputs (and the chunk CRCs right behind them) back to the staging
-    const size_t back = ncrc ? crc_off + ncrc * sizeof(uint32_t) - pitch * nlive : pitch * (nout - 1) + lj;
-    hipError_t e = hipSuccess;
-    if (!zc) {
-      e = hipMemcpyAsync(h.pin + pitch * nlive, h.dev + pitch * nlive, back, hipMemcpyDeviceToHost, h.stream);
-      if (e != hipSuccess) return hip_fail(c, e, "hipMemcpyAsync D2H");
-    }
-    e = hipEventRecord(h.done, h.stream);
-    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
-    pending[sl] = true;
-    pend_off[sl] = off;
-    pend_len[sl] = lj;
-  }
-  for (size_t j = nchunks > static_cast<size_t>(nslots) ? nchunks - nslots : 0; j < nchunks; ++j) {
-    hrs_status st = finish(static_cast<int>(j % nslots));
-    if (st != HRS_OK) return st;
-  }
-  return HRS_OK;
+  return st;
 }
 
 // A call that fails part-way may leave a slot's H2D / kernel / D2H in

@@ -71,7 +71,7 @@ const char* last_kernel();
 constexpr int kBatchMaxIn = 32;  // > 16 inputs (or > 8 with 6-8 outputs): batch_stream_kernel
 constexpr int kHostBatchSlots = 3;  // chunk slots of the host-memory batch pipeline
 constexpr int kAsyncSlots = 4;      // operations in flight per handle (hrs_*_submit / hrs_collect)
-constexpr int kHostSlots = 4;       // chunk slots of a synchronous host-buffer call (at most; HRS_HOST_SLOTS)
+constexpr int kHostSlots = 8;       // chunk slots of a synchronous host-buffer call (at most; HRS_HOST_SLOTS)
 struct BatchPlan {            // one erasure pattern, a device table entry
   int nin;                    // live survivor rows read
   int nout;                   // erased rows written
@@ -94,6 +94,13 @@ struct BatchArgs {
 };
 
 hipError_t launch_batch_bitsliced(const BatchArgs& a, int max_nout, int max_nin, hipStream_t s);
+
+// ---- stream gates of the queued host pipeline (hrs_gate.hip)
+// gate: waits until *ready (a coherent pinned word the host writes) reaches
+// `want` (serial-number order), or `timeout` wall-clock ticks pass (then *fail
+// = 1). signal: *done = tag with a system-scope release.
+hipError_t launch_gate(const uint32_t* ready, uint32_t want, uint32_t* fail, uint64_t timeout, hipStream_t s);
+hipError_t launch_signal(uint32_t* done, uint32_t tag, hipStream_t s);
 hipError_t launch_batch_bytewise(const BatchArgs& a, hipStream_t s);
 
 }  // namespace hrs

@@ -392,4 +392,5 @@ def test_host_call_fuzz(cuda):
         if not all(np.array_equal(outs[j], want[j]) for j in range(len(erased))):
             raise AssertionError(_fz_report(case, fam, k, p, L_, gap, rows, outs, want, erased, ntr, paths[-1]))
         assert all(np.array_equal(rows[x], src[x]) for x in range(n)), case  # the reads are left as they were
-    assert set(paths) <= {"staged", "pinned"}, paths
+    # ragged rows and chunks no one-pass CRC kernel takes use the copy engine
+    assert set(paths) <= {"staged", "pinned", "copy_engine"}, paths

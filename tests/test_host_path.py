@@ -11,16 +11,29 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine"])
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "gated"])
 def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
     bytes: the staged zero-copy path (the default: rows copied into pinned
     staging, the kernel works on the staging across the link) and the copy
-    engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H). Which caller memory runs in place
+    engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H), and the gated
+    queue (HRS_HOST_GATE=1, 128 KiB chunks after a 64 KiB first one over 4
+    slots: every chunk's kernels queued ahead behind gate kernels the host
+    opens after each copy-in). Which caller memory runs in place
     (runtime-pinned only) is test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
+    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST"):
+        monkeypatch.delenv(var, raising=False)
     if request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
+        monkeypatch.setenv("HRS_HOST_GATE", "0")
+    elif request.param == "gated":  # gated queued chunks, small and many (hrs_hostpath.cpp staged_run)
+        monkeypatch.setenv("HRS_HOST_GATE", "1")
+        monkeypatch.setenv("HRS_HOST_CHUNK", "131072")
+        monkeypatch.setenv("HRS_HOST_SLOTS", "4")
+        monkeypatch.setenv("HRS_HOST_FIRST", "65536")
+    else:
+        monkeypatch.setenv("HRS_HOST_GATE", "0")
     return request.param
 
 
@@ -93,3 +106,37 @@ def test_host_calls_on_pinned_rows(cuda, transfer_mode, L):
     assert dcrc == [zlib.crc32(data[2].tobytes(), 9)]
     if L % 2048 == 0:  # a ragged checksummed repair has no one-pass kernel: it is staged
         assert code.lastHostPath() == want_path
+
+
+def test_gate_miss_reruns_without_gates(cuda, transfer_mode, monkeypatch):
+    """A gate that gives up waiting (its host stalled past the timeout; test
+    hooks HRS_GATE_TIMEOUT_US / HRS_GATE_DELAY_US) lets its chunk's kernels
+    run on stale staging; the call must notice the miss, discard those
+    results and run again without gates: bit-exact outputs and CRCs."""
+    import time
+    import zlib
+    if transfer_mode != "gated":
+        pytest.skip("gated queue only")
+    k, p, L = 10, 4, 1 << 20
+    code = HipReedSolomonCode(k, p, zero_inputs_after_encode=False)
+    rng = np.random.default_rng(77)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    par = [np.zeros(L, np.uint8) for _ in range(p)]
+    ref = C.encode_bulk(k, p, data)
+    code.encodeBulk(data, par)  # first run of these chunk shapes: no gates yet
+    code.encodeBulkCrc(data, par)
+    monkeypatch.setenv("HRS_GATE_TIMEOUT_US", "200")
+    monkeypatch.setenv("HRS_GATE_DELAY_US", "20000")
+    for x in par:
+        x[:] = 0xC3
+    t0 = time.perf_counter()
+    code.encodeBulk(data, par)
+    assert time.perf_counter() - t0 >= 0.02  # the stall happened inside the gated run
+    assert all((a == b).all() for a, b in zip(par, ref))
+    for x in par:
+        x[:] = 0x3C
+    run = [int(v) for v in rng.integers(0, 1 << 32, k + p, dtype=np.uint64)]
+    crcs = code.encodeBulkCrc(data, par, run)
+    assert all((a == b).all() for a, b in zip(par, ref))
+    cells = data + list(ref)
+    assert crcs == [zlib.crc32(cells[i].tobytes(), run[i]) & 0xFFFFFFFF for i in range(k + p)]
