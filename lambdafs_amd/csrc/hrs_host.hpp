@@ -52,8 +52,8 @@ class CopyPool {
     }
     Batch b;
     for (const CopyJob& j : jobs)
-      for (size_t off = 0; off < j.bytes; off += kPiece) {
-        const size_t n = std::min(kPiece, j.bytes - off);
+      for (size_t off = 0; off < j.bytes; off += piece_) {
+        const size_t n = std::min(piece_, j.bytes - off);
         b.pieces.push_back({static_cast<uint8_t*>(j.dst) + off, static_cast<const uint8_t*>(j.src) + off, n});
       }
     {
@@ -63,6 +63,11 @@ class CopyPool {
     }
     cv_.notify_all();
     drain(b);
+    // the last pieces are in other threads' hands: spin a while before
+    // sleeping (a condition-variable wake-up costs about a piece's copy)
+    const auto t0 = std::chrono::steady_clock::now();
+    while (b.done.load(std::memory_order_acquire) != b.pieces.size() && std::chrono::steady_clock::now() - t0 < kSpin)
+      __builtin_ia32_pause();
     std::unique_lock<std::mutex> lk(mu_);
     close(&b);  // no new worker may join
     done_cv_.wait(lk, [&] { return b.users == 0 && b.done.load() == b.pieces.size(); });
@@ -78,7 +83,24 @@ class CopyPool {
   }
 
  private:
-  static constexpr size_t kPiece = 256u << 10;
+  // A synchronous call holds the pool for its duration (Hold): its copy-ins
+  // and copy-outs come every few tens of microseconds, and a worker woken
+  // through the condition variable joins a batch that late (round 6 trace: a
+  // 2.5 MiB copy-in took 35-50 us, single-thread speed). While any call holds
+  // the pool, idle workers spin instead of sleeping.
+ public:
+  class Hold {
+   public:
+    Hold() : p_(CopyPool::instance()) { p_.holders_.fetch_add(1, std::memory_order_acq_rel); }
+    ~Hold() { p_.holders_.fetch_sub(1, std::memory_order_acq_rel); }
+    Hold(const Hold&) = delete;
+    Hold& operator=(const Hold&) = delete;
+
+   private:
+    CopyPool& p_;
+  };
+
+ private:
 
   struct Batch {
     std::vector<CopyJob> pieces;
@@ -113,6 +135,11 @@ class CopyPool {
     if (n < 0) n = 0;
     if (n > 32) n = 32;
     nthreads_ = n;
+    // Piece size: the unit a thread claims (HRS_HOST_PIECE, bytes; default
+    // 64 KiB: a 2.5 MiB copy-in splits into 40 pieces over the threads)
+    const char* pe = getenv("HRS_HOST_PIECE");
+    const long pc = pe ? atol(pe) : 0;
+    piece_ = pc >= 4096 ? static_cast<size_t>(pc) : static_cast<size_t>(64) << 10;
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker(); });
   }
 
@@ -140,7 +167,8 @@ class CopyPool {
 
   void spin_for_work() {
     const auto t0 = std::chrono::steady_clock::now();
-    while (nopen_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() - t0 < kSpin)
+    while (nopen_.load(std::memory_order_acquire) == 0 &&
+           (holders_.load(std::memory_order_acquire) > 0 || std::chrono::steady_clock::now() - t0 < kSpin))
       __builtin_ia32_pause();
   }
 
@@ -170,6 +198,8 @@ class CopyPool {
   }
 
   int nthreads_ = 0;
+  size_t piece_ = static_cast<size_t>(64) << 10;
+  std::atomic<int> holders_{0};  // calls holding the pool (Hold): idle workers spin
   std::vector<std::thread> threads_;
   std::vector<Batch*> open_;
   std::atomic<size_t> nopen_{0};  // open_.size(), readable without mu_ (spin_for_work)

@@ -260,19 +260,24 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   std::vector<uint32_t> parts(static_cast<size_t>(ncrc) * C);
   std::vector<const uint8_t*> din(nin);
   std::vector<uint8_t*> dout(nout);
+  hrs::CopyPool::Hold hold;  // the pool's workers stay awake for this call
+  // Copies go to the pool as one batch per step: the outputs of every chunk
+  // that is done (copy_out) and the next chunk's inputs (copy_in). A chunk's
+  // input rows and output rows are disjoint regions of its slot, so a chunk's
+  // copy-out and its slot's next copy-in may share a batch.
   auto copy_in = [&](size_t j) {
     const hrs_codec::HostSlot& h = c->host[j % S];
-    jobs.clear();
     for (int i = 0; i < nin; ++i)
       if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + ch[j].off, ch[j].len});
-    pool.run(jobs);
   };
   auto copy_out = [&](size_t j) {
     const hrs_codec::HostSlot& h = c->host[j % S];
-    jobs.clear();
     for (int o = 0; o < nout; ++o) jobs.push_back({out_rows[o] + ch[j].off, h.pin + pitch * (nlive + o), ch[j].len});
-    pool.run(jobs);
     if (ncrc) std::memcpy(&parts[j * ncrc], h.pin + crc_off, ncrc * sizeof(uint32_t));
+  };
+  auto flush = [&] {
+    if (!jobs.empty()) pool.run(jobs);
+    jobs.clear();
   };
   // the chunk's kernels (and, off the zero-copy path, its H2D and D2H) on its slot's stream
   auto launch = [&](size_t j) -> hrs_status {
@@ -348,16 +353,20 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
         if (st == HRS_OK) copy_out(out_next++);
       }
       if (st != HRS_OK) break;
+      while (out_next < j && done(out_next)) copy_out(out_next++);
       copy_in(j);
+      flush();
       if (j == 1 && delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
       __atomic_store_n(flag_ready(c, static_cast<int>(j % S)), tag(j), __ATOMIC_RELEASE);
       if (j + S < C) st = enqueue(j + S);
-      while (st == HRS_OK && out_next < j && done(out_next)) copy_out(out_next++);
     }
     while (st == HRS_OK && out_next < C) {
       st = wait_done(out_next);
       if (st == HRS_OK) copy_out(out_next++);
+      while (out_next < C && done(out_next)) copy_out(out_next++);
+      flush();
     }
+    jobs.clear();
     if (st != HRS_OK) {  // open every gate of this call so its queued work drains
       for (int sl = 0; sl < S; ++sl) __atomic_store_n(flag_ready(c, sl), tag0 + static_cast<uint32_t>(C), __ATOMIC_RELEASE);
       return st;
@@ -370,22 +379,25 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   } else {
     auto ev = [&](size_t j) { return c->host[j % S].done; };
     for (size_t j = 0; j < C; ++j) {
-      while (out_next + S <= j) {
+      while (out_next + S <= j) {  // the slot's previous chunk must be out
         hipError_t e = hipEventSynchronize(ev(out_next));
         if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
         copy_out(out_next++);
       }
+      while (out_next < j && hipEventQuery(ev(out_next)) == hipSuccess) copy_out(out_next++);
       copy_in(j);
+      flush();
       st = launch(j);
       if (st != HRS_OK) return st;
       hipError_t e = hipEventRecord(ev(j), c->host[j % S].stream);
       if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
-      while (out_next < j && hipEventQuery(ev(out_next)) == hipSuccess) copy_out(out_next++);
     }
     while (out_next < C) {
       hipError_t e = hipEventSynchronize(ev(out_next));
       if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
       copy_out(out_next++);
+      while (out_next < C && hipEventQuery(ev(out_next)) == hipSuccess) copy_out(out_next++);
+      flush();
     }
   }
   if (c->staged_shapes.size() > 256) c->staged_shapes.clear();

@@ -6,7 +6,8 @@
 // one RS(k,p) stripe of L-byte pageable rows (default RS(10,4), 1 MiB).
 // Every variant's parity, CRCs and repaired row must equal the first
 // variant's (and the repaired row the lost one), or the tool fails.
-// Usage: host_pipeline_sweep [calls] [rounds] [L]   (one JSON line per variant, medians)
+// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate,...]
+//   (one JSON line per variant, medians)
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
@@ -19,21 +20,36 @@
 #include "../include/hrs.h"
 
 struct Variant {
-  const char* name;
-  const char* chunk;
-  const char* slots;
-  const char* first;
-  const char* gate;
+  std::string name, chunk, slots, first, gate;
 };
 
-static const Variant kVariants[] = {
-    {"c512_s2", "524288", "2", "0", "0"},          {"c256_s4", "262144", "4", "0", "0"},
-    {"c128_s4", "131072", "4", "0", "0"},          {"c128_s8", "131072", "8", "0", "0"},
-    {"c512_s2_gate", "524288", "2", "0", "1"},     {"c256_s2_gate", "262144", "2", "0", "1"},
-    {"c256_s4_gate", "262144", "4", "0", "1"},     {"c128_s4_gate", "131072", "4", "0", "1"},
-    {"c128_s8_gate", "131072", "8", "0", "1"},     {"c256_s4_f64_gate", "262144", "4", "65536", "1"},
-    {"c128_s4_f64_gate", "131072", "4", "65536", "1"},
-};
+// Default variants; argv[4] may list others as name:chunk:slots:first:gate,...
+static std::vector<Variant> default_variants() {
+  return {{"c512_s2", "524288", "2", "0", "0"},      {"c256_s4", "262144", "4", "0", "0"},
+          {"c128_s4", "131072", "4", "0", "0"},      {"c128_s8", "131072", "8", "0", "0"},
+          {"c512_s2_gate", "524288", "2", "0", "1"}, {"c256_s2_gate", "262144", "2", "0", "1"},
+          {"c256_s4_gate", "262144", "4", "0", "1"}, {"c128_s4_gate", "131072", "4", "0", "1"}};
+}
+
+static std::vector<Variant> parse_variants(const char* spec) {
+  std::vector<Variant> v;
+  std::string s(spec);
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    std::string item = s.substr(pos, end - pos), f[5];
+    size_t q = 0;
+    for (int i = 0; i < 5; ++i) {
+      size_t c = item.find(':', q);
+      f[i] = item.substr(q, c == std::string::npos ? std::string::npos : c - q);
+      q = c == std::string::npos ? item.size() : c + 1;
+    }
+    v.push_back({f[0], f[1], f[2], f[3], f[4]});
+    pos = end + 1;
+  }
+  return v;
+}
 
 int main(int argc, char** argv) {
   const int calls = argc > 1 ? atoi(argv[1]) : 100;
@@ -71,7 +87,8 @@ int main(int argc, char** argv) {
   std::vector<const uint8_t*> reads(n, nullptr);
   // the parity rows are read after the first encode has filled them
   std::vector<uint32_t> crc(n), dcrc(1);
-  const int nv = static_cast<int>(sizeof kVariants / sizeof kVariants[0]);
+  const std::vector<Variant> kVariants = argc > 4 ? parse_variants(argv[4]) : default_variants();
+  const int nv = static_cast<int>(kVariants.size());
   std::vector<std::vector<double>> t(nv * 4);
   std::vector<std::string> paths(nv);
   std::vector<uint8_t> ref_par;
@@ -87,10 +104,10 @@ int main(int argc, char** argv) {
   for (int rd = 0; rd < rounds; ++rd)
     for (int v = 0; v < nv; ++v) {
       const Variant& V = kVariants[v];
-      setenv("HRS_HOST_CHUNK", V.chunk, 1);
-      setenv("HRS_HOST_SLOTS", V.slots, 1);
-      setenv("HRS_HOST_FIRST", V.first, 1);
-      setenv("HRS_HOST_GATE", V.gate, 1);
+      setenv("HRS_HOST_CHUNK", V.chunk.c_str(), 1);
+      setenv("HRS_HOST_SLOTS", V.slots.c_str(), 1);
+      setenv("HRS_HOST_FIRST", V.first.c_str(), 1);
+      setenv("HRS_HOST_GATE", V.gate.c_str(), 1);
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
@@ -98,7 +115,7 @@ int main(int argc, char** argv) {
       for (int r = 0; r < p; ++r) got.insert(got.end(), par[r], par[r] + L);
       if (ref_par.empty()) ref_par = got;
       if (got != ref_par) {
-        fprintf(stderr, "%s: parity differs from %s\n", V.name, kVariants[0].name);
+        fprintf(stderr, "%s: parity differs from %s\n", V.name.c_str(), kVariants[0].name.c_str());
         ok = false;
       }
       for (int i = 0; i < nr; ++i) reads[to_read[i]] = rows[to_read[i]].data();
@@ -108,14 +125,14 @@ int main(int argc, char** argv) {
                          L) == HRS_OK;
       }));
       if (memcmp(lost.data(), rows[p].data(), L) != 0) {
-        fprintf(stderr, "%s: repaired row differs\n", V.name);
+        fprintf(stderr, "%s: repaired row differs\n", V.name.c_str());
         ok = false;
       }
       t[v * 4 + 2].push_back(
           time_it([&] { ok &= hrs_encode_crc(c, in.data(), par.data(), L, nullptr, crc.data()) == HRS_OK; }));
       if (ref_crc.empty()) ref_crc = crc;
       if (crc != ref_crc) {
-        fprintf(stderr, "%s: encode CRCs differ\n", V.name);
+        fprintf(stderr, "%s: encode CRCs differ\n", V.name.c_str());
         ok = false;
       }
       memset(lostp, 0, L);
@@ -125,7 +142,7 @@ int main(int argc, char** argv) {
       }));
       if (rd == 0 && v == 0) ref_dcrc = dcrc[0];
       if (dcrc[0] != ref_dcrc || memcmp(lost.data(), rows[p].data(), L) != 0) {
-        fprintf(stderr, "%s: decode CRC or repaired row differs\n", V.name);
+        fprintf(stderr, "%s: decode CRC or repaired row differs\n", V.name.c_str());
         ok = false;
       }
     }
@@ -137,7 +154,8 @@ int main(int argc, char** argv) {
     printf("{\"variant\": \"%s\", \"chunk\": %s, \"slots\": %s, \"first\": %s, \"gate\": %s, \"path\": \"%s\", "
            "\"L\": %zu, \"calls\": %d, \"rounds\": %d, \"encode_ms\": %.4f, \"decode_ms\": %.4f, \"encode_crc_ms\": %.4f, "
            "\"decode_crc_ms\": %.4f, \"ok\": %s}\n",
-           kVariants[v].name, kVariants[v].chunk, kVariants[v].slots, kVariants[v].first, kVariants[v].gate,
+           kVariants[v].name.c_str(), kVariants[v].chunk.c_str(), kVariants[v].slots.c_str(), kVariants[v].first.c_str(),
+           kVariants[v].gate.c_str(),
            paths[v].c_str(), L, calls, rounds, med(t[v * 4]), med(t[v * 4 + 1]), med(t[v * 4 + 2]), med(t[v * 4 + 3]),
            ok ? "true" : "false");
   hrs_destroy(c);
