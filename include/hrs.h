@@ -110,12 +110,15 @@ const char* hrs_last_error(const hrs_codec* codec);
 const char* hrs_last_kernel(const hrs_codec* codec);
 /* How the handle's latest synchronous host-buffer call (hrs_encode, hrs_decode,
  * hrs_decode3, hrs_*_crc) or host batch (hrs_*_batch_host) moved its bytes:
- * "pinned" (rows or batch in the caller's pinned memory: the zero-copy kernel
- * in place), "staged" (pageable memory copied through pinned staging, the
- * zero-copy kernel on the staging; the default), "direct" (opt-in,
- * HRS_HOST_DIRECT=1: pageable memory registered for the call, the kernel in
- * place), "copy_engine" (staging, H2D, kernel, D2H), or "" before any such
- * call. Diagnostic, like hrs_last_kernel. */
+ * "pinned" (rows or batch in memory the runtime allocated pinned —
+ * hipHostMalloc, torch pin_memory —: the zero-copy kernel in place),
+ * "staged" (any other host memory, pageable or registered by the caller with
+ * hipHostRegister, copied through the library's pinned staging, the zero-copy
+ * kernel on the staging; the default), "copy_engine" (staging, H2D, kernel,
+ * D2H), or "" before any such call. The GPU never reads or writes
+ * caller-registered pageable memory in place: registration does not pin its
+ * pages ("Platform constraint"). Diagnostic, like
+ * hrs_last_kernel. */
 const char* hrs_last_host_path(const hrs_codec* codec);
 const char* hrs_version(void);
 
@@ -315,11 +318,13 @@ hrs_status hrs_decode_batch_dev(hrs_codec* codec, const uint8_t* stripes, size_t
  * stripe, Decoder.java:232-401). The stripes flow in chunks through a ring of
  * device slots, each on its own stream: H2D of exactly the rows the chunk's
  * code reads, the kernel, D2H of exactly the rows it writes, successive chunks
- * overlapping. Buffers allocated pinned (hipHostMalloc, hipHostRegister, torch
- * pin_memory) are DMA'd directly and the whole job is queued at once;
- * pageable buffers are staged through the handle's pinned slots by the copy
- * pool. Synchronous: outputs are in place when the call returns. Rows need no
- * alignment. */
+ * overlapping. Buffers the runtime allocated pinned (hipHostMalloc, torch
+ * pin_memory) are used in place (zero copy; or DMA'd directly with
+ * HRS_ZEROCOPY=0) and the whole job is queued at once; any other buffer —
+ * pageable, or pageable memory the caller registered with hipHostRegister,
+ * whose pages are not pinned — is staged through the handle's pinned slots by
+ * the copy pool. Synchronous: outputs are in place when the call returns.
+ * Rows need no alignment. */
 
 /* hrs_decode_batch_dev over host memory (same layout, semantics and errors):
  * stripe s holds location l at stripes + s * stripe_stride + l * row_stride;

@@ -13,11 +13,24 @@
 package io.hops.erasure_coding;
 
 import java.io.IOException;
+import java.io.UncheckedIOException;
 import java.util.Arrays;
 import org.apache.hadoop.conf.Configurable;
 import org.apache.hadoop.conf.Configuration;
 
-public class HipReedSolomonCode extends ErasureCode implements Configurable {
+/*
+ * Extends ReedSolomonCode itself, so it is a drop-in wherever the reference
+ * code or its tests expect that class: `instanceof ReedSolomonCode`
+ * (TestCodec.java:119), the cast to reach the 3-arg decodeBulk
+ * (TestNativeErasureCodes.java:100), and the inherited Java
+ * computeErrorLocations (ReedSolomonCode.java:243-287; its inner decode call
+ * runs on the GPU through the override below). super.init sets up the
+ * reference's own small tables for that method; every bulk byte is still
+ * computed by libhrs.so. ReedSolomonCode's bulk methods declare no checked
+ * exceptions, so an engine failure surfaces as UncheckedIOException (its
+ * cause the IOException the shim threw), as the scalar methods already did.
+ */
+public class HipReedSolomonCode extends ReedSolomonCode implements Configurable {
   private long nativeCodec;  // hrs_codec*, owned (cf. jni_common.c:35-70 "nativeCoder")
   private int stripeSize;
   private int paritySize;
@@ -55,11 +68,13 @@ public class HipReedSolomonCode extends ErasureCode implements Configurable {
 
   @Deprecated
   public HipReedSolomonCode(int stripeSize, int paritySize) {
+    super(stripeSize, paritySize);  // the reference's tables (computeErrorLocations)
     init(stripeSize, paritySize);
   }
 
   @Override
   public void init(Codec codec) {  // ReedSolomonCode.java:48-54
+    super.init(codec);  // the reference's tables (computeErrorLocations)
     init(codec.stripeLength, codec.parityLength);
   }
 
@@ -72,10 +87,14 @@ public class HipReedSolomonCode extends ErasureCode implements Configurable {
 
   /** Same result as ReedSolomonCode.encodeBulk (ReedSolomonCode.java:103-125). */
   @Override
-  public void encodeBulk(byte[][] inputs, byte[][] outputs) throws IOException {
+  public void encodeBulk(byte[][] inputs, byte[][] outputs) {
     assert (stripeSize == inputs.length);
     assert (paritySize == outputs.length);
-    HrsNative.encode(nativeCodec, inputs, outputs, outputs[0].length);
+    try {
+      HrsNative.encode(nativeCodec, inputs, outputs, outputs[0].length);
+    } catch (IOException e) {
+      throw new UncheckedIOException(e);
+    }
     // The Java bulk remainder zeroes its inputs (GaloisField.java:326-338); keep that contract.
     for (byte[] in : inputs) {
       Arrays.fill(in, (byte) 0);
@@ -155,21 +174,29 @@ public class HipReedSolomonCode extends ErasureCode implements Configurable {
   /** Same result as ReedSolomonCode.decodeBulk 5-arg (ReedSolomonCode.java:191-211). */
   @Override
   public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocations,
-      int[] locationsToRead, int[] locationsNotToRead) throws IOException {
+      int[] locationsToRead, int[] locationsNotToRead) {
     if (erasedLocations.length == 0) {
       return;
     }
-    HrsNative.decode(nativeCodec, readBufs, writeBufs, erasedLocations, locationsToRead,
-        locationsNotToRead, readBufs[0].length);
+    try {
+      HrsNative.decode(nativeCodec, readBufs, writeBufs, erasedLocations, locationsToRead,
+          locationsNotToRead, readBufs[0].length);
+    } catch (IOException e) {
+      throw new UncheckedIOException(e);
+    }
   }
 
   /** Same result as ReedSolomonCode.decodeBulk 3-arg (ReedSolomonCode.java:168-185). */
-  public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocation)
-      throws IOException {
+  @Override
+  public void decodeBulk(byte[][] readBufs, byte[][] writeBufs, int[] erasedLocation) {
     if (erasedLocation.length == 0) {
       return;
     }
-    HrsNative.decode3(nativeCodec, readBufs, writeBufs, erasedLocation, readBufs[0].length);
+    try {
+      HrsNative.decode3(nativeCodec, readBufs, writeBufs, erasedLocation, readBufs[0].length);
+    } catch (IOException e) {
+      throw new UncheckedIOException(e);
+    }
   }
 
   @Override
