@@ -22,7 +22,7 @@ JNI      := lambdafs_amd/libhrs_jni.so
 HARNESS  := tests/cpp/codec_harness tests/cpp/crc_model tests/cpp/jni_harness tests/cpp/host_logic tests/cpp/crc_tables \
             tests/cpp/copy_pool_test
 
-TOOLS    := tools/host_call_rate tools/host_pipeline_sweep
+TOOLS    := tools/host_call_rate tools/host_pipeline_sweep tools/host_copy_probe
 
 all: $(LIB) $(PROBE) $(ORACLE) $(JNI) $(HARNESS) $(TOOLS)
 
@@ -33,6 +33,10 @@ tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
 # A/B of the staged pipeline's knobs, interleaved in one process (profiles/r06/).
 tools/host_pipeline_sweep: tools/host_pipeline_sweep.cpp include/hrs.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
+
+# Host copy rates of the staging copies on the box's CPUs (profiles/r06/).
+tools/host_copy_probe: tools/host_copy_probe.cpp lambdafs_amd/csrc/hrs_host.hpp
+	$(HIPCC) -O2 -std=c++17 -Wall -pthread -o $@ $<
 
 $(API_OBJ): build/%.o: lambdafs_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p build

@@ -26,6 +26,7 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
 #include <sched.h>
 
 namespace hrs {
@@ -34,7 +35,43 @@ struct CopyJob {
   void* dst;
   const void* src;
   size_t bytes;
+  bool stream = false;  // nontemporal stores: dst is read next by a device, not by this CPU
 };
+
+// memcpy with nontemporal (streaming) stores: the destination lines go to
+// memory instead of this CPU's caches, so a device reading them next across
+// the host link does not snoop them out of a CPU cache, and the copy does not
+// evict the caller's working set. AVX2 where the CPU has it, else memcpy.
+__attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const uint8_t* s, size_t n) {
+  const size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
+  if (head >= n) {
+    std::memcpy(d, s, n);
+    return;
+  }
+  std::memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+  }
+  std::memcpy(d + i, s + i, n - i);
+  _mm_sfence();  // the streamed lines are in memory before this copy counts as done
+}
+
+inline void copy_job(void* d, const void* s, size_t n, bool stream) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (stream && avx2)
+    stream_copy_avx2(static_cast<uint8_t*>(d), static_cast<const uint8_t*>(s), n);
+  else
+    std::memcpy(d, s, n);
+}
 
 class CopyPool {
  public:
@@ -47,14 +84,14 @@ class CopyPool {
     size_t total = 0;
     for (const CopyJob& j : jobs) total += j.bytes;
     if (nthreads_ == 0 || total < (256u << 10)) {
-      for (const CopyJob& j : jobs) std::memcpy(j.dst, j.src, j.bytes);
+      for (const CopyJob& j : jobs) copy_job(j.dst, j.src, j.bytes, j.stream);
       return;
     }
     Batch b;
     for (const CopyJob& j : jobs)
       for (size_t off = 0; off < j.bytes; off += piece_) {
         const size_t n = std::min(piece_, j.bytes - off);
-        b.pieces.push_back({static_cast<uint8_t*>(j.dst) + off, static_cast<const uint8_t*>(j.src) + off, n});
+        b.pieces.push_back({static_cast<uint8_t*>(j.dst) + off, static_cast<const uint8_t*>(j.src) + off, n, j.stream});
       }
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -148,7 +185,7 @@ class CopyPool {
     for (;;) {
       const size_t i = b.next.fetch_add(1);
       if (i >= b.pieces.size()) return;
-      std::memcpy(b.pieces[i].dst, b.pieces[i].src, b.pieces[i].bytes);
+      copy_job(b.pieces[i].dst, b.pieces[i].src, b.pieces[i].bytes, b.pieces[i].stream);
       b.done.fetch_add(1);
     }
   }

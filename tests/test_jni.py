@@ -76,8 +76,29 @@ def test_java_codecs_take_a_device_from_the_conf():
     assert "static native int deviceCount()" in nat
     dev = open(os.path.join(jdir, "HipDevices.java")).read()
     assert 'DEVICES_KEY = "hdfs.raid.hip.devices"' in dev
+    parent = {"HipReedSolomonCode": "ReedSolomonCode", "HipXORCode": "ErasureCode",
+              "HipNativeReedSolomonCode": "ErasureCode", "HipSimpleRegeneratingCode": "ErasureCode"}
     for cls in ("HipReedSolomonCode", "HipXORCode", "HipNativeReedSolomonCode", "HipSimpleRegeneratingCode"):
         src = open(os.path.join(jdir, cls + ".java")).read()
-        assert f"public class {cls} extends ErasureCode implements Configurable" in src, cls
+        assert f"public class {cls} extends {parent[cls]} implements Configurable" in src, cls
         assert "public void setConf(Configuration conf)" in src and "HipDevices.pick(conf)" in src, cls
         assert "HrsNative.create(" not in src.replace("return HrsNative.create(", ""), cls  # only via the wrapper
+
+
+def test_java_rs_codec_is_a_reedsolomoncode():
+    """HipReedSolomonCode extends ReedSolomonCode (VERDICT r5 missing #4):
+    `instanceof ReedSolomonCode` (TestCodec.java:119) and the cast to reach the
+    3-arg decodeBulk (TestNativeErasureCodes.java:100) hold, and the Java
+    computeErrorLocations (ReedSolomonCode.java:243-287) is inherited with the
+    reference's tables set up by super.init. Overrides of methods
+    ReedSolomonCode declares without checked exceptions must not add one (a
+    javac error): the bulk overrides wrap the shim's IOException. No JDK here:
+    a source check."""
+    src = open(os.path.join(ROOT, "lambdafs_amd", "jni", "HipReedSolomonCode.java")).read()
+    assert "super.init(codec);" in src and "super(stripeSize, paritySize);" in src
+    for sig in (r"public void encodeBulk\(byte\[\]\[\] inputs, byte\[\]\[\] outputs\)\s*\{",
+                r"public void decodeBulk\(byte\[\]\[\] readBufs, byte\[\]\[\] writeBufs, int\[\] erasedLocations,"
+                r"\s*int\[\] locationsToRead, int\[\] locationsNotToRead\)\s*\{",
+                r"public void decodeBulk\(byte\[\]\[\] readBufs, byte\[\]\[\] writeBufs, int\[\] erasedLocation\)\s*\{"):
+        assert re.search(sig, src), sig
+    assert src.count("throw new UncheckedIOException(e);") >= 3

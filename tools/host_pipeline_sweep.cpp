@@ -1,12 +1,13 @@
 // A/B sweep of the staged synchronous host-buffer pipeline's knobs
 // (hrs_hostpath.cpp staged_run: HRS_HOST_CHUNK, HRS_HOST_SLOTS,
-// HRS_HOST_FIRST, HRS_HOST_GATE, all read per call), interleaved round by
+// HRS_HOST_FIRST, HRS_HOST_GATE, HRS_HOST_QUEUE / HRS_HOST_QCHUNK, all read
+// per call), interleaved round by
 // round in one process over the four calls the JNI shim makes per Encoder /
 // Decoder round: hrs_encode / hrs_decode / hrs_encode_crc / hrs_decode_crc on
 // one RS(k,p) stripe of L-byte pageable rows (default RS(10,4), 1 MiB).
 // Every variant's parity, CRCs and repaired row must equal the first
 // variant's (and the repaired row the lost one), or the tool fails.
-// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate,...]
+// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate[:nt],...]
 //   (one JSON line per variant, medians)
 #include <algorithm>
 #include <chrono>
@@ -20,7 +21,7 @@
 #include "../include/hrs.h"
 
 struct Variant {
-  std::string name, chunk, slots, first, gate;
+  std::string name, chunk, slots, first, gate, nt = "0";
 };
 
 // Default variants; argv[4] may list others as name:chunk:slots:first:gate,...
@@ -38,14 +39,14 @@ static std::vector<Variant> parse_variants(const char* spec) {
   while (pos < s.size()) {
     size_t end = s.find(',', pos);
     if (end == std::string::npos) end = s.size();
-    std::string item = s.substr(pos, end - pos), f[5];
+    std::string item = s.substr(pos, end - pos), f[6] = {"", "", "", "", "", "0"};
     size_t q = 0;
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < 6 && q < item.size(); ++i) {
       size_t c = item.find(':', q);
       f[i] = item.substr(q, c == std::string::npos ? std::string::npos : c - q);
       q = c == std::string::npos ? item.size() : c + 1;
     }
-    v.push_back({f[0], f[1], f[2], f[3], f[4]});
+    v.push_back({f[0], f[1], f[2], f[3], f[4], f[5]});
     pos = end + 1;
   }
   return v;
@@ -107,7 +108,13 @@ int main(int argc, char** argv) {
       setenv("HRS_HOST_CHUNK", V.chunk.c_str(), 1);
       setenv("HRS_HOST_SLOTS", V.slots.c_str(), 1);
       setenv("HRS_HOST_FIRST", V.first.c_str(), 1);
-      setenv("HRS_HOST_GATE", V.gate.c_str(), 1);
+      // gate 2 = the queued pipeline (one gated launch per call, HRS_HOST_QUEUE,
+      // chunk -> HRS_HOST_QCHUNK); 0 / 1 = the chunked pipeline without / with gate kernels
+      const bool queued = V.gate == "2";
+      setenv("HRS_HOST_QUEUE", queued ? "1" : "0", 1);
+      setenv("HRS_HOST_QCHUNK", V.chunk.c_str(), 1);
+      setenv("HRS_HOST_GATE", queued ? "0" : V.gate.c_str(), 1);
+      setenv("HRS_HOST_NT", V.nt.c_str(), 1);
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
@@ -151,12 +158,11 @@ int main(int argc, char** argv) {
     return v[v.size() / 2];
   };
   for (int v = 0; v < nv; ++v)
-    printf("{\"variant\": \"%s\", \"chunk\": %s, \"slots\": %s, \"first\": %s, \"gate\": %s, \"path\": \"%s\", "
+    printf("{\"variant\": \"%s\", \"chunk\": %s, \"slots\": %s, \"first\": %s, \"gate\": %s, \"nt\": %s, \"path\": \"%s\", "
            "\"L\": %zu, \"calls\": %d, \"rounds\": %d, \"encode_ms\": %.4f, \"decode_ms\": %.4f, \"encode_crc_ms\": %.4f, "
            "\"decode_crc_ms\": %.4f, \"ok\": %s}\n",
            kVariants[v].name.c_str(), kVariants[v].chunk.c_str(), kVariants[v].slots.c_str(), kVariants[v].first.c_str(),
-           kVariants[v].gate.c_str(),
-           paths[v].c_str(), L, calls, rounds, med(t[v * 4]), med(t[v * 4 + 1]), med(t[v * 4 + 2]), med(t[v * 4 + 3]),
+           kVariants[v].gate.c_str(), kVariants[v].nt.c_str(), paths[v].c_str(), L, calls, rounds, med(t[v * 4]), med(t[v * 4 + 1]), med(t[v * 4 + 2]), med(t[v * 4 + 3]),
            ok ? "true" : "false");
   hrs_destroy(c);
   return ok ? 0 : 1;
