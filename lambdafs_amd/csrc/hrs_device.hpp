@@ -178,8 +178,15 @@ __device__ __forceinline__ bool gate_wait(const Gate& g, uint64_t t, uint32_t& s
   if (static_cast<int32_t>(seen - need) >= 0) return true;
   const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
   for (;;) {
-    seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(g.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
-    if (static_cast<int32_t>(seen - need) >= 0) return true;
+    // poll relaxed (an acquire per poll would invalidate the L2 under every
+    // other wave), then one acquire once the chunk is in: staging lines a
+    // previous call left in the L2 must not be read (g.uncached: the staging
+    // is coherent host memory the GPU does not cache, no fence needed)
+    seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(g.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (static_cast<int32_t>(seen - need) >= 0) {
+      if (!g.uncached) __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      return true;
+    }
     if (static_cast<uint64_t>(wall_clock64()) - t0 > g.timeout) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(g.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;

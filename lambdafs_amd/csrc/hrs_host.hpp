@@ -166,17 +166,20 @@ class CopyPool {
 
   CopyPool() {
     const char* e = getenv("HRS_HOST_THREADS");
-    // default: half the CPU share, 2..8 threads (tools/bench_host_ab.py and
-    // bench_hbatch.py sweeps, profiles/r04/NOTES.md)
-    int n = e ? atoi(e) : std::min(8, std::max(2, cpu_share() / 2));
+    // default 2 workers (1 on a share under 4 CPUs): the caller plus two
+    // threads already reach what one CPU complex moves (the MI355X boxes give
+    // a job 16 CPUs of one CCD: ~77 GB/s copy on one thread, ~95-105 with the
+    // pool); more spinning workers only contend for it: RS(10,4) 1 MiB encode
+    // 0.280 ms with 2, 0.335 with 4, 0.37 with 8 (profiles/r06/NOTES.md)
+    int n = e ? atoi(e) : (cpu_share() >= 4 ? 2 : 1);
     if (n < 0) n = 0;
     if (n > 32) n = 32;
     nthreads_ = n;
     // Piece size: the unit a thread claims (HRS_HOST_PIECE, bytes; default
-    // 64 KiB: a 2.5 MiB copy-in splits into 40 pieces over the threads)
+    // 256 KiB, measured ahead of 64 and 32 KiB, profiles/r06/NOTES.md)
     const char* pe = getenv("HRS_HOST_PIECE");
     const long pc = pe ? atol(pe) : 0;
-    piece_ = pc >= 4096 ? static_cast<size_t>(pc) : static_cast<size_t>(64) << 10;
+    piece_ = pc >= 4096 ? static_cast<size_t>(pc) : static_cast<size_t>(256) << 10;
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker(); });
   }
 
@@ -235,7 +238,7 @@ class CopyPool {
   }
 
   int nthreads_ = 0;
-  size_t piece_ = static_cast<size_t>(64) << 10;
+  size_t piece_ = static_cast<size_t>(256) << 10;
   std::atomic<int> holders_{0};  // calls holding the pool (Hold): idle workers spin
   std::vector<std::thread> threads_;
   std::vector<Batch*> open_;

@@ -158,13 +158,17 @@ static size_t env_window_bytes(const char* name, size_t dflt) {
   return static_cast<size_t>(x) / hrs::kWindowBytes * hrs::kWindowBytes;
 }
 
-size_t host_chunk_bytes() { return env_window_bytes("HRS_HOST_CHUNK", 512 << 10); }
+// Defaults measured with tools/host_pipeline_sweep (profiles/r06/NOTES.md):
+// plain calls 256 KiB x 4 slots (RS(10,4) 1 MiB encode 0.280 ms against
+// 0.312 at 512 KiB x 2), checksummed calls 512 KiB x 2 (each chunk also
+// launches its CRC fold: fewer, larger chunks win there, 0.337 vs 0.348).
+size_t host_chunk_bytes(bool crc) { return env_window_bytes("HRS_HOST_CHUNK", (crc ? 512 : 256) << 10); }
 size_t host_first_bytes(size_t chunk) { return std::min(chunk, env_window_bytes("HRS_HOST_FIRST", chunk)); }
 
-int host_slots() {
+int host_slots(bool crc) {
   const char* e = getenv("HRS_HOST_SLOTS");
   const int x = e ? atoi(e) : 0;
-  return (x >= 2 && x <= hrs::kHostSlots) ? x : 2;
+  return (x >= 2 && x <= hrs::kHostSlots) ? x : (crc ? 2 : 4);
 }
 
 // Copy-ins into the staging with nontemporal stores (HRS_HOST_NT, read per
@@ -217,7 +221,7 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   struct Span {
     size_t off, len;
   };
-  const size_t chunk = std::min(len, host_chunk_bytes());
+  const size_t chunk = std::min(len, host_chunk_bytes(crc.mode != kCrcNone));
   const size_t first = host_first_bytes(chunk);
   std::vector<Span> ch;
   for (size_t off = 0; off < len;) {
@@ -226,7 +230,7 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     off += l;
   }
   const size_t C = ch.size();
-  const int S = static_cast<int>(std::min<size_t>(host_slots(), C));
+  const int S = static_cast<int>(std::min<size_t>(host_slots(crc.mode != kCrcNone), C));
   const size_t pitch = pitch_for(chunk);
   // slot layout: nlive + nout rows of `pitch`, then (CRC only) the chunk's
   // ncrc CRC words, then the raw window-CRC scratch (device side only)
@@ -439,6 +443,11 @@ bool host_queue_on() {
   return e && e[0] == '1';
 }
 
+bool host_queue_uncached() {
+  const char* e = getenv("HRS_HOST_QUC");
+  return e && e[0] == '1';
+}
+
 constexpr size_t kQueueMaxLen = static_cast<size_t>(16) << 20;  // longer rows take the chunked pipeline
 
 bool done_flags(hrs_codec* c, size_t words) {
@@ -480,6 +489,28 @@ hrs_status queued_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   if (st != HRS_OK) return st;
   hrs_codec::HostSlot& h = c->host[0];
   if (!h.pin_dev || !gate_flags(c) || !done_flags(c, len / hrs::kWindowBytes)) return HRS_OK;
+  // HRS_HOST_QUC=1 (A/B): the staging in coherent host memory the GPU does not
+  // cache (no acquire after a gate; the pinned slot's device buffer still
+  // holds the raw CRC scratch)
+  const bool uc = host_queue_uncached();
+  uint8_t* pin = h.pin;
+  if (uc) {
+    if (c->qpin_bytes < need) {
+      if (c->qpin) (void)hipHostFree(c->qpin);  // no call of this handle is in flight
+      c->qpin = nullptr;
+      c->qpin_bytes = 0;
+      void* p = nullptr;
+      if (hipHostMalloc(&p, need, hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        return HRS_OK;
+      }
+      c->qpin = static_cast<uint8_t*>(p);
+      c->qpin_bytes = need;
+    }
+    uint8_t* d = nullptr;
+    if (!host_device_ptr(c->qpin, need, &d)) return HRS_OK;
+    pin = c->qpin;
+  }
   *taken = true;
   c->last_host_path = "staged";
   const uint64_t key = static_cast<uint64_t>(4 + crc.mode) << 56 | static_cast<uint64_t>(len);
@@ -494,17 +525,17 @@ hrs_status queued_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   auto copy_in = [&](size_t j) {
     const size_t off = j * chunk, lj = std::min(chunk, len - off);
     for (int i = 0; i < nin; ++i)
-      if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i] + off, in_rows[i] + off, lj});
+      if (slot_of[i] >= 0) jobs.push_back({pin + pitch * slot_of[i] + off, in_rows[i] + off, lj});
   };
   auto copy_out = [&](size_t j) {
     const size_t off = j * chunk, lj = std::min(chunk, len - off);
-    for (int o = 0; o < nout; ++o) jobs.push_back({out_rows[o] + off, h.pin + pitch * (nlive + o) + off, lj});
+    for (int o = 0; o < nout; ++o) jobs.push_back({out_rows[o] + off, pin + pitch * (nlive + o) + off, lj});
   };
   std::vector<const uint8_t*> din(nin);
   std::vector<uint8_t*> dout(nout);
-  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? h.pin_dev + pitch * slot_of[i] : nullptr;
-  for (int o = 0; o < nout; ++o) dout[o] = h.pin_dev + pitch * (nlive + o);
-  uint32_t* dcrc = reinterpret_cast<uint32_t*>(h.pin_dev + crc_off);
+  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? pin + pitch * slot_of[i] : nullptr;  // device = host address
+  for (int o = 0; o < nout; ++o) dout[o] = pin + pitch * (nlive + o);
+  uint32_t* dcrc = reinterpret_cast<uint32_t*>(pin + crc_off);
   uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
   auto enqueue = [&]() -> hrs_status {
     hrs::GridCap cap(zero_copy_blocks());
@@ -530,6 +561,7 @@ hrs_status queued_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     ctx.proto.done = c->qdone;
     ctx.proto.fail = flag_fail(c);
     ctx.proto.timeout = c->gate_timeout;
+    ctx.proto.uncached = uc ? 1u : 0u;
     const char* te = getenv("HRS_GATE_TIMEOUT_US");  // test hooks, as staged_run's
     if (te && atol(te) > 0) ctx.proto.timeout = c->gate_timeout / 10000000u * static_cast<uint64_t>(atol(te));
     const char* de = getenv("HRS_GATE_DELAY_US");
@@ -611,7 +643,7 @@ hrs_status queued_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     if (out_next < C) return fail(c, HRS_EDEVICE, "queued call: chunks left unflagged without a gate miss");
   }
   if (ncrc) {  // CRC32.update chaining from the running values
-    const uint32_t* part = reinterpret_cast<const uint32_t*>(h.pin + crc_off);
+    const uint32_t* part = reinterpret_cast<const uint32_t*>(pin + crc_off);
     const hrs::crc::Mat& z = crc_zmat(c, len);
     for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[r];
   }

@@ -39,8 +39,8 @@ struct Gate {
   uint64_t timeout;
   uint32_t tag;
   uint32_t done_tag;
-  uint32_t tpc;  // tasks per chunk
-  uint32_t pad_;
+  uint32_t tpc;       // tasks per chunk
+  uint32_t uncached;  // 1: the staging is coherent host memory the GPU does not cache
 };
 
 struct RowArgs {

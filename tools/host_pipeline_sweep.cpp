@@ -114,7 +114,8 @@ int main(int argc, char** argv) {
       setenv("HRS_HOST_QUEUE", queued ? "1" : "0", 1);
       setenv("HRS_HOST_QCHUNK", V.chunk.c_str(), 1);
       setenv("HRS_HOST_GATE", queued ? "0" : V.gate.c_str(), 1);
-      setenv("HRS_HOST_NT", V.nt.c_str(), 1);
+      setenv("HRS_HOST_NT", queued ? "0" : V.nt.c_str(), 1);
+      setenv("HRS_HOST_QUC", queued ? V.nt.c_str() : "0", 1);  // queued: the nt field selects coherent staging
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
