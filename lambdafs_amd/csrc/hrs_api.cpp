@@ -196,8 +196,6 @@ void hrs_destroy(hrs_codec* c) {
     if (h.pin) (void)hipHostFree(h.pin);
   }
   if (c->qflags) (void)hipHostFree(c->qflags);  // every slot stream has drained above
-  if (c->qdone) (void)hipHostFree(c->qdone);
-  if (c->qpin) (void)hipHostFree(c->qpin);
   for (auto& a : c->async) {
     if (a.stream) {
       (void)hipStreamSynchronize(a.stream);

@@ -196,8 +196,6 @@ hipError_t launch_batch_n(const BatchArgs& a, hipStream_t s) {
   auto kern = use_pat_prefetch() ? batch_bitsliced_kernel<NOUT, NINB, true> : batch_bitsliced_kernel<NOUT, NINB, false>;
   note_kernel_t("batch_bitsliced_kernel", NOUT, NINB, use_pat_prefetch());
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
-  const hipError_t ge = gate_other(s);
-  if (ge != hipSuccess) return ge;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderBatch));
   return hipGetLastError();
 }
@@ -207,8 +205,6 @@ hipError_t launch_batch_stream_n(const BatchArgs& a, hipStream_t s) {
   auto kern = batch_stream_kernel<NOUT, 4>;
   note_kernel_t("batch_stream_kernel", NOUT, 4);
   const int per_cu = NOUT >= 4 ? 3 : 2;
-  const hipError_t ge = gate_other(s);
-  if (ge != hipSuccess) return ge;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderBatch));
   return hipGetLastError();
 }
@@ -245,8 +241,6 @@ hipError_t launch_batch_bitsliced(const BatchArgs& a, int max_nout, int max_nin,
 hipError_t launch_batch_bytewise(const BatchArgs& a, hipStream_t s) {
   const unsigned g = grid_for(batch_bytewise_kernel, kBlockThreads, a.ntasks);
   note_kernel("batch_bytewise_kernel");
-  const hipError_t ge = gate_other(s);
-  if (ge != hipSuccess) return ge;
   hipLaunchKernelGGL(batch_bytewise_kernel, dim3(g), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }

@@ -81,13 +81,6 @@ struct hrs_codec {
   uint32_t qtag = 0;
   uint64_t gate_timeout = 0;
   std::set<uint64_t> staged_shapes;
-  // queued pipeline (hrs_hostpath.cpp queued_run): per-window done flags
-  // (coherent pinned) and the next done tag (never 0)
-  uint32_t* qdone = nullptr;
-  size_t qdone_words = 0;
-  uint32_t qdone_next = 1;
-  uint8_t* qpin = nullptr;  // coherent staging of the queued pipeline (HRS_HOST_QUC=1)
-  size_t qpin_bytes = 0;
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
   // its own compute stream; every slot's H2D goes on one copy-in stream and

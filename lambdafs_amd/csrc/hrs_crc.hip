@@ -155,8 +155,6 @@ hipError_t launch_crc_windows(const CrcWinArgs& a, bool aligned, int cus, hipStr
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(shm));
   if (e != hipSuccess) return e;
-  const hipError_t ge = gate_other(s);
-  if (ge != hipSuccess) return ge;
   hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(g)), dim3(kCrcBlockThreads), shm, s, with_order(a, kOrderCrc));
   return hipGetLastError();
 }
@@ -168,9 +166,6 @@ hipError_t launch_crc_fold(const CrcFoldArgs& a, int cus, hipStream_t s) {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm));
   if (e != hipSuccess) return e;
   note_kernel("crc_fold_kernel");
-  // the fold reads the raw window CRCs the (gated) kernel before it on the
-  // stream wrote, so the stream orders it: no gate of its own. It writes no
-  // output rows; the host reads its CRCs after the call's end event.
   hipLaunchKernelGGL(crc_fold_kernel, dim3(g), dim3(256), shm, s, a);
   return hipGetLastError();
 }

@@ -92,7 +92,6 @@ struct EncodeCrcArgs {
   int pad_;
   uint32_t* raw;
   const uint32_t* tables;  // kCrcLdsWordsA words (device)
-  Gate gate;               // queued host pipeline (hrs_internal.hpp; set at launch)
 };
 
 // family: kStaticRs / kStaticCauchy (hrs_internal.hpp). *handled = false when

@@ -107,36 +107,23 @@ __global__ void __launch_bounds__(kDecCrcThreads) decode_crc_pipe_kernel(const D
   asm volatile("" : "+s"(nin));
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
   uint32_t j = 0;
-  uint32_t seen = a.gate.tag;  // queued host pipeline: a task's chunk is waited for before its loads
   uint64_t t = wt.at(0);
   if (t >= wt.end) return;
   uint32_t ra[NINB][8], rb[NINB][8];
   uint32_t acc[NOUT][8];
-  if (!gate_wait(a.gate, t, seen)) return;
   dc_load_task<NOUT, NINB>(a, t, nin, lane, ra);
   uint64_t t1 = wt.at(++j);
-  if (t1 < wt.end) {
-    if (!gate_wait(a.gate, t1, seen)) return;
-    dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
-  }
+  if (t1 < wt.end) dc_load_task<NOUT, NINB>(a, t1, nin, lane, rb);
   for (;;) {  // ra: task t, rb: task t1 in flight; every wave leaves once a task index passes its end
     dc_apply_task<NOUT, NINB>(a, t, nin, lane, ra, acc);
     const uint64_t t2 = wt.at(++j);
-    if (t2 < wt.end) {
-      if (!gate_wait(a.gate, t2, seen)) return;
-      dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
-    }
+    if (t2 < wt.end) dc_load_task<NOUT, NINB>(a, t2, nin, lane, ra);
     dc_crc_task<NOUT, DPP>(d, t, lane, slices, zchunk, tree, acc);
-    gate_done(a.gate, t);
     if (t1 >= wt.end) break;
     dc_apply_task<NOUT, NINB>(a, t1, nin, lane, rb, acc);
     const uint64_t t3 = wt.at(++j);
-    if (t3 < wt.end) {
-      if (!gate_wait(a.gate, t3, seen)) return;
-      dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
-    }
+    if (t3 < wt.end) dc_load_task<NOUT, NINB>(a, t3, nin, lane, rb);
     dc_crc_task<NOUT, DPP>(d, t1, lane, slices, zchunk, tree, acc);
-    gate_done(a.gate, t1);
     if (t2 >= wt.end) break;
     t = t2;
     t1 = t3;
@@ -169,11 +156,9 @@ __global__ void __launch_bounds__(THREADS) decode_crc_kernel(const DecodeCrcArgs
   const uint32_t* zchunk = lds + kCrcSliceWords;
   const uint32_t* tree = zchunk + 1024;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  uint32_t seen = a.gate.tag;  // queued host pipeline (gate_wait)
   for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
     const uint64_t t = wt.at(j);
     if (t >= wt.end) break;
-    if (!gate_wait(a.gate, t, seen)) return;
     int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
     asm volatile("" : "+s"(nin));
     // written out, not through dc_load_task / dc_apply_task: with the helpers
@@ -200,7 +185,6 @@ __global__ void __launch_bounds__(THREADS) decode_crc_kernel(const DecodeCrcArgs
       store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
     }
     dc_crc_task<NOUT, true>(d, t, lane, slices, zchunk, tree, acc);
-    gate_done(a.gate, t);
   }
 }
 
@@ -219,8 +203,6 @@ template <int NOUT, int NINB>
 hipError_t launch_dc(const DecodeCrcArgs& d, int cus, hipStream_t s) {
   DecodeCrcArgs dc = d;
   dc.r.order = task_order(kOrderDecodeCrc);
-  const hipError_t ge = gate_rows(dc.r, s);
-  if (ge != hipSuccess) return ge;
   if constexpr (NOUT >= 2) {
     const int threads = dcrc_threads();
     auto kern = threads == 768 ? decode_crc_kernel<NOUT, NINB, 768> : decode_crc_kernel<NOUT, NINB, 512>;

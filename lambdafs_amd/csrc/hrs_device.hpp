@@ -165,43 +165,6 @@ __device__ __forceinline__ WaveTasks wave_tasks(uint64_t ntasks, int order) {
   return {lo + w, lo + per < ntasks ? lo + per : ntasks, 0, 0xFFFFFFFFu, wpb};
 }
 
-// ------------------------------------------------ queued-pipeline gates
-// (Gate, hrs_internal.hpp). Wave-uniform: every lane calls them together.
-// `seen` caches the latest *ready the wave read (start it at g.tag), so a wave
-// reads the flag across the link once per chunk it needs, not once per task;
-// the acquire that read performs makes the chunk's staging visible to the
-// wave's loads. False: the chunk did not arrive within g.timeout (*fail set):
-// the wave must leave the kernel.
-__device__ __forceinline__ bool gate_wait(const Gate& g, uint64_t t, uint32_t& seen) {
-  if (!g.ready) return true;
-  const uint32_t need = g.tag + static_cast<uint32_t>(t / g.tpc) + 1u;
-  if (static_cast<int32_t>(seen - need) >= 0) return true;
-  const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-  for (;;) {
-    // poll relaxed (an acquire per poll would invalidate the L2 under every
-    // other wave), then one acquire once the chunk is in: staging lines a
-    // previous call left in the L2 must not be read (g.uncached: the staging
-    // is coherent host memory the GPU does not cache, no fence needed)
-    seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(g.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    if (static_cast<int32_t>(seen - need) >= 0) {
-      if (!g.uncached) __atomic_thread_fence(__ATOMIC_ACQUIRE);
-      return true;
-    }
-    if (static_cast<uint64_t>(wall_clock64()) - t0 > g.timeout) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store(g.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// After the task's stores: done[t] = done_tag. The release orders the wave's
-// stores (all lanes: the wait it implies is per wave) before the flag.
-__device__ __forceinline__ void gate_done(const Gate& g, uint64_t t) {
-  if (g.ready && (threadIdx.x & 63) == 0)
-    __hip_atomic_store(g.done + t, g.done_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // mask[o][r][q]: the input bit-planes of data row r that feed bit-plane q of
 // parity row o (gf::row_mask of G[o][r]). Evaluated by the compiler.
 // MATRIX is gf::EncodeMatrix<K,P> (hops RS) or gf::CauchyMatrix<K,P> (nrs).

@@ -18,7 +18,6 @@
 #include "crc32.hpp"
 #include "hrs_crc.hpp"
 #include "hrs_internal.hpp"
-#include "hrs_launch.hpp"
 
 namespace hrs::api {
 
@@ -58,7 +57,6 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
   const uint64_t tail = len - tail_off;
 
   if (live.empty()) {  // all-zero matrix: outputs are zero
-    if (hrs::t_gate) ++hrs::t_gate->other;  // queued pipeline: no done flags cover these rows
     for (int o = 0; o < nout; ++o)
       for (size_t st = 0; st < nstripes; ++st) {
         hipError_t e = hipMemsetAsync(out_rows[o] + st * out_stride, 0, len, s);

@@ -167,11 +167,9 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
   const uint32_t* tree = zchunk + 1024;
   const uint64_t ntasks = a.nstripes * a.nwin;
   const WaveTasks wt = wave_tasks(ntasks, a.order);
-  uint32_t seen = a.gate.tag;  // queued host pipeline (gate_wait)
   for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
     const uint64_t t = wt.at(j);
     if (t >= wt.end) break;
-    if (!gate_wait(a.gate, t, seen)) return;
     const uint64_t stripe = t / a.nwin;
     const uint64_t w = t - stripe * a.nwin;
     const uint64_t in_base = stripe * a.in_stride + w * a.subs * kWindowBytes;
@@ -247,7 +245,6 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
       const uint32_t c = lane_tree(tree, crc[r]);
       if (lane == 0) a.raw[(stripe * N + r) * a.nwin + w] = c;
     }
-    gate_done(a.gate, t);
   }
 }
 
@@ -327,11 +324,7 @@ hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   uint64_t g = (ntasks + per_block - 1) / per_block;
   if (g > static_cast<uint64_t>(cus)) g = cus;
   g = capped_grid(g);  // zero-copy calls cap it (hrs::GridCap)
-  EncodeCrcArgs b = with_order(a, kOrderFusedEncode);
-  e = k.sched < 0 ? gate_other(s)  // the row-serial A/B kernel has no gate
-                  : gate_args(b.gate, static_cast<uint64_t>(a.subs) * kWindowBytes, a.nstripes, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k.k, dim3(static_cast<unsigned>(g)), dim3(k.threads), shm, s, b);
+  hipLaunchKernelGGL(k.k, dim3(static_cast<unsigned>(g)), dim3(k.threads), shm, s, with_order(a, kOrderFusedEncode));
   return hipGetLastError();
 }
 

@@ -149,8 +149,10 @@ bool host_apply_pinned(hrs_codec* c, const uint8_t* m, int nout, int nin, const 
 // each behind a gate kernel that waits for the chunk's tag in a pinned flag
 // word (hrs_gate.hip) and followed by a signal kernel the host polls; the host
 // publishes the tag as soon as the copy-in ends, so no launch sits between a
-// chunk's copy-in and its kernel. Without gates a chunk is launched after its
-// copy-in and its completion is an event.
+// chunk's copy-in and its kernel. Measured slower (each gate / signal
+// dispatch costs the slot stream more than the launch latency it hides:
+// profiles/r06/NOTES.md), so it is an A/B knob; by default a chunk is
+// launched after its copy-in and its completion is an event.
 static size_t env_window_bytes(const char* name, size_t dflt) {
   const char* e = getenv(name);
   const long x = e ? atol(e) : 0;
@@ -421,235 +423,6 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   return HRS_OK;
 }
 
-// ---- the queued pipeline (pageable rows, HRS_HOST_QUEUE) ----
-// One launch covers the whole call: the kernel is queued over the call's
-// full-length staging rows BEFORE anything is copied, its waves gated per
-// chunk in the kernel itself (Gate, hrs_internal.hpp: a wave waits for its
-// window's chunk on a pinned flag the host bumps after each copy-in, and flags
-// each window done after its stores). The host copies chunk after chunk in
-// (HRS_HOST_QCHUNK bytes of every row, 128 KiB by default) and copies each
-// chunk out as soon as all its windows are flagged, so the link starts after
-// the first small chunk and only the last chunk's copy-out follows it; no
-// launch, event or stream switch per chunk. Kernels or operations the gates do
-// not cover (tails, other families) wait behind a gate kernel for the last
-// chunk and the host then waits for the call's end event: still correct, not
-// overlapped. A call whose shape has not run before runs once ungated (copies
-// first): it creates any CRC tables outside the gated window. A wave that
-// gives up waiting (10 s) makes the call re-run on the chunked pipeline.
-size_t host_queue_chunk() { return env_window_bytes("HRS_HOST_QCHUNK", 128 << 10); }
-
-bool host_queue_on() {
-  const char* e = getenv("HRS_HOST_QUEUE");
-  return e && e[0] == '1';
-}
-
-bool host_queue_uncached() {
-  const char* e = getenv("HRS_HOST_QUC");
-  return e && e[0] == '1';
-}
-
-constexpr size_t kQueueMaxLen = static_cast<size_t>(16) << 20;  // longer rows take the chunked pipeline
-
-bool done_flags(hrs_codec* c, size_t words) {
-  if (c->qdone_words >= words) return true;
-  if (c->qdone) (void)hipHostFree(c->qdone);  // no call of this handle is in flight
-  c->qdone = nullptr;
-  c->qdone_words = 0;
-  void* p = nullptr;
-  if (hipHostMalloc(&p, words * sizeof(uint32_t), hipHostMallocCoherent) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  uint8_t* d = nullptr;
-  if (!host_device_ptr(p, words * sizeof(uint32_t), &d)) {
-    (void)hipHostFree(p);
-    return false;
-  }
-  std::memset(p, 0, words * sizeof(uint32_t));  // done tags are never 0
-  c->qdone = static_cast<uint32_t*>(p);
-  c->qdone_words = words;
-  return true;
-}
-
-hrs_status queued_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
-                      uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc, int ncrc,
-                      const std::vector<int>& slot_of, int nlive, bool* taken, bool* missed) {
-  *taken = false;
-  *missed = false;
-  if (!zero_copy_on() || len > kQueueMaxLen || len % hrs::kWindowBytes) return HRS_OK;
-  if (crc.mode == kCrcEncode && !encode_crc_one_pass(c, len, 1)) return HRS_OK;
-  if (crc.mode == kCrcOutputs && !apply_crc_one_pass(c, nout, nlive, len)) return HRS_OK;
-  const size_t chunk = std::min(len, host_queue_chunk());
-  const size_t C = (len + chunk - 1) / chunk;
-  const size_t pitch = pitch_for(len);
-  const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
-  const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
-  const size_t need = ncrc ? raw_off + crc_raw_bytes_for(len, 1, ncrc) : crc_off;
-  hrs_status st = host_slot(c, 0, need);
-  if (st != HRS_OK) return st;
-  hrs_codec::HostSlot& h = c->host[0];
-  if (!h.pin_dev || !gate_flags(c) || !done_flags(c, len / hrs::kWindowBytes)) return HRS_OK;
-  // HRS_HOST_QUC=1 (A/B): the staging in coherent host memory the GPU does not
-  // cache (no acquire after a gate; the pinned slot's device buffer still
-  // holds the raw CRC scratch)
-  const bool uc = host_queue_uncached();
-  uint8_t* pin = h.pin;
-  if (uc) {
-    if (c->qpin_bytes < need) {
-      if (c->qpin) (void)hipHostFree(c->qpin);  // no call of this handle is in flight
-      c->qpin = nullptr;
-      c->qpin_bytes = 0;
-      void* p = nullptr;
-      if (hipHostMalloc(&p, need, hipHostMallocCoherent) != hipSuccess) {
-        (void)hipGetLastError();
-        return HRS_OK;
-      }
-      c->qpin = static_cast<uint8_t*>(p);
-      c->qpin_bytes = need;
-    }
-    uint8_t* d = nullptr;
-    if (!host_device_ptr(c->qpin, need, &d)) return HRS_OK;
-    pin = c->qpin;
-  }
-  *taken = true;
-  c->last_host_path = "staged";
-  const uint64_t key = static_cast<uint64_t>(4 + crc.mode) << 56 | static_cast<uint64_t>(len);
-  const bool gated = c->staged_shapes.count(key) > 0;
-  hrs::CopyPool& pool = hrs::CopyPool::instance();
-  hrs::CopyPool::Hold hold;
-  std::vector<hrs::CopyJob> jobs;
-  auto flush = [&] {
-    if (!jobs.empty()) pool.run(jobs);
-    jobs.clear();
-  };
-  auto copy_in = [&](size_t j) {
-    const size_t off = j * chunk, lj = std::min(chunk, len - off);
-    for (int i = 0; i < nin; ++i)
-      if (slot_of[i] >= 0) jobs.push_back({pin + pitch * slot_of[i] + off, in_rows[i] + off, lj});
-  };
-  auto copy_out = [&](size_t j) {
-    const size_t off = j * chunk, lj = std::min(chunk, len - off);
-    for (int o = 0; o < nout; ++o) jobs.push_back({out_rows[o] + off, pin + pitch * (nlive + o) + off, lj});
-  };
-  std::vector<const uint8_t*> din(nin);
-  std::vector<uint8_t*> dout(nout);
-  for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? pin + pitch * slot_of[i] : nullptr;  // device = host address
-  for (int o = 0; o < nout; ++o) dout[o] = pin + pitch * (nlive + o);
-  uint32_t* dcrc = reinterpret_cast<uint32_t*>(pin + crc_off);
-  uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
-  auto enqueue = [&]() -> hrs_status {
-    hrs::GridCap cap(zero_copy_blocks());
-    if (crc.mode == kCrcEncode) return encode_crc_impl(c, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, h.stream, draw);
-    if (crc.mode == kCrcOutputs)
-      return apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, nullptr, dcrc, h.stream, draw);
-    return run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, len, 1, h.stream, static_kp);
-  };
-  if (!gated) {  // first run of this shape: copies, then the launches (no gates)
-    for (size_t j = 0; j < C; ++j) copy_in(j);
-    flush();
-    st = enqueue();
-    if (st != HRS_OK) return st;
-    hipError_t e = hipStreamSynchronize(h.stream);
-    if (e != hipSuccess) return hip_fail(c, e, "hipStreamSynchronize");
-    for (size_t j = 0; j < C; ++j) copy_out(j);
-    flush();
-    if (c->staged_shapes.size() > 256) c->staged_shapes.clear();
-    c->staged_shapes.insert(key);
-  } else {
-    hrs::GateCtx ctx{};
-    ctx.proto.ready = flag_ready(c, 0);
-    ctx.proto.done = c->qdone;
-    ctx.proto.fail = flag_fail(c);
-    ctx.proto.timeout = c->gate_timeout;
-    ctx.proto.uncached = uc ? 1u : 0u;
-    const char* te = getenv("HRS_GATE_TIMEOUT_US");  // test hooks, as staged_run's
-    if (te && atol(te) > 0) ctx.proto.timeout = c->gate_timeout / 10000000u * static_cast<uint64_t>(atol(te));
-    const char* de = getenv("HRS_GATE_DELAY_US");
-    const long delay_us = de ? atol(de) : 0;
-    const uint32_t tag = c->qtag;
-    c->qtag += static_cast<uint32_t>(C) + 1u;
-    ctx.proto.tag = tag;
-    ctx.chunk_bytes = chunk;
-    ctx.nchunks = static_cast<uint32_t>(C);
-    ctx.next_done = c->qdone_next;
-    hrs::t_gate = &ctx;
-    st = enqueue();
-    hrs::t_gate = nullptr;
-    c->qdone_next = ctx.next_done + 1u;
-    if (c->qdone_next == 0) c->qdone_next = 1;  // 0 is the flags' initial value
-    auto open_all = [&] { __atomic_store_n(flag_ready(c, 0), tag + static_cast<uint32_t>(C), __ATOMIC_RELEASE); };
-    if (st != HRS_OK) {
-      open_all();
-      return st;
-    }
-    hipError_t e = hipEventRecord(h.done, h.stream);
-    if (e != hipSuccess) {
-      open_all();
-      return hip_fail(c, e, "hipEventRecord");
-    }
-    // the done flags cover the outputs when every output-writing launch was gated
-    const bool per_window = ctx.gated > 0 && ctx.other == 0 && ctx.last_tpc > 0;
-    const uint32_t final_tag = ctx.last_done;
-    const size_t tpc = ctx.last_tpc ? ctx.last_tpc : 1;
-    const size_t ntasks = len / (chunk / tpc);
-    size_t scan = 0;  // windows [0, scan) are done
-    auto chunk_done = [&](size_t j) {
-      const size_t end = std::min((j + 1) * tpc, ntasks);
-      while (scan < end && __atomic_load_n(c->qdone + scan, __ATOMIC_ACQUIRE) == final_tag) ++scan;
-      return scan >= end;
-    };
-    size_t out_next = 0;
-    for (size_t j = 0; j < C; ++j) {
-      while (per_window && out_next < j && chunk_done(out_next)) copy_out(out_next++);
-      copy_in(j);
-      flush();
-      if (j == 1 && delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
-      __atomic_store_n(flag_ready(c, 0), tag + static_cast<uint32_t>(j) + 1u, __ATOMIC_RELEASE);
-    }
-    bool ended = false;
-    while (out_next < C) {
-      if (!per_window || ended) {
-        e = hipEventSynchronize(h.done);
-        if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
-        if (per_window && !chunk_done(C - 1)) break;  // a wave gave up: the fail flag says so below
-        while (out_next < C) copy_out(out_next++);
-        flush();
-        break;
-      }
-      if (chunk_done(out_next)) {
-        while (out_next < C && chunk_done(out_next)) copy_out(out_next++);
-        flush();
-        continue;
-      }
-      for (uint32_t spin = 1; !chunk_done(out_next); ++spin) {
-        if ((spin & 1023u) == 0) {  // the kernel ended without flagging this chunk, or failed
-          e = hipEventQuery(h.done);
-          if (e == hipSuccess) {
-            ended = true;
-            break;
-          }
-          if (e != hipErrorNotReady) return hip_fail(c, e, "queued call");
-        }
-        __builtin_ia32_pause();
-      }
-    }
-    e = hipEventSynchronize(h.done);  // the CRC fold, and nothing of this call left on the staging
-    if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
-    if (__atomic_load_n(flag_fail(c), __ATOMIC_ACQUIRE)) {
-      __atomic_store_n(flag_fail(c), 0u, __ATOMIC_RELEASE);
-      *missed = true;
-      return HRS_OK;
-    }
-    if (out_next < C) return fail(c, HRS_EDEVICE, "queued call: chunks left unflagged without a gate miss");
-  }
-  if (ncrc) {  // CRC32.update chaining from the running values
-    const uint32_t* part = reinterpret_cast<const uint32_t*>(pin + crc_off);
-    const hrs::crc::Mat& z = crc_zmat(c, len);
-    for (int r = 0; r < ncrc; ++r) crc.out[r] = hrs::crc::apply(z, crc.out[r]) ^ part[r];
-  }
-  return HRS_OK;
-}
-
 hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                            uint8_t* const* out_rows, size_t len, bool static_kp, const HostCrc& crc) {
   const int ncrc = crc.mode == kCrcEncode ? nin + nout : crc.mode == kCrcOutputs ? nout : 0;
@@ -677,15 +450,9 @@ hrs_status host_apply_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, co
     if (host_apply_pinned(c, m, nout, nin, live_rows.data(), out_rows, len, static_kp, crc, ncrc, &st)) return st;
   }
   std::vector<uint32_t> start(crc.out, crc.out + ncrc);  // crc.out may alias crc.in: kept for a re-run
-  bool missed = false, taken = false;
-  hrs_status st = HRS_OK;
-  if (host_queue_on())
-    st = queued_run(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc, ncrc, slot_of, nlive, &taken, &missed);
-  if (st != HRS_OK) return st;
-  if (taken && !missed) return HRS_OK;
-  if (missed) std::copy(start.begin(), start.end(), crc.out);
-  st = staged_run(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc, ncrc, slot_of, nlive,
-                  host_gate_on(), &missed);
+  bool missed = false;
+  hrs_status st = staged_run(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc, ncrc, slot_of, nlive,
+                             host_gate_on(), &missed);
   if (st == HRS_OK && missed) {  // a gate gave up waiting: discard everything and run it without gates
     std::copy(start.begin(), start.end(), crc.out);
     st = staged_run(c, m, nout, nin, in_rows, out_rows, len, static_kp, crc, ncrc, slot_of, nlive, false, &missed);

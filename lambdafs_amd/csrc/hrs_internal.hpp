@@ -23,26 +23,6 @@ constexpr int kWindowBytes = 2048;
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 
-// In-kernel gate of the queued host pipeline (hrs_hostpath.cpp queued_run):
-// one launch covers a whole synchronous call whose inputs the host copies
-// into the pinned staging chunk by chunk. Task t (a window of the call's one
-// stripe) belongs to chunk t / tpc, which is in once *ready >= tag + chunk + 1
-// (serial-number order); a wave waits for it before loading the task (at most
-// `timeout` wall-clock ticks, then *fail = 1 and the wave leaves), and after
-// the task's stores sets done[t] = done_tag with a system-scope release, so
-// the host copies each chunk out as soon as its windows are done.
-// ready == nullptr: no gate (every launch outside that pipeline).
-struct Gate {
-  const uint32_t* ready;
-  uint32_t* done;
-  uint32_t* fail;
-  uint64_t timeout;
-  uint32_t tag;
-  uint32_t done_tag;
-  uint32_t tpc;       // tasks per chunk
-  uint32_t uncached;  // 1: the staging is coherent host memory the GPU does not cache
-};
-
 struct RowArgs {
   const uint8_t* in[kMaxIn];
   uint8_t* out[kMaxOut];
@@ -56,7 +36,6 @@ struct RowArgs {
   int nout;
   int accumulate;                 // 1: XOR into existing outputs (input chunking)
   int order;                      // window -> wave order (hrs_launch.hpp task_order), set at launch
-  Gate gate;                      // queued host pipeline (set at launch; null otherwise)
 };
 
 inline void set_coef(RowArgs& a, int o, int i, uint8_t v) {

@@ -47,11 +47,9 @@ template <int K, int P, class MATRIX>
 __device__ __forceinline__ void encode_static_body(const RowArgs& a) {
   const int lane = threadIdx.x & 63;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  uint32_t seen = a.gate.tag;  // queued host pipeline (gate_wait); no gate: a.gate.ready == nullptr
   for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
     const uint64_t t = wt.at(j);
     if (t >= wt.end) break;
-    if (!gate_wait(a.gate, t, seen)) return;
     const uint64_t stripe = t / a.nwin;
     const uint64_t off = (t - stripe * a.nwin) * kWindowBytes;
     uint32_t acc[P][8];
@@ -82,7 +80,6 @@ __device__ __forceinline__ void encode_static_body(const RowArgs& a) {
       bitslice(acc[o]);
       store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
     }
-    gate_done(a.gate, t);
   }
 }
 
@@ -177,10 +174,7 @@ hipError_t launch_static(const RowArgs& a, hipStream_t s) {
   auto kern = encode_static_kernel<K, P>;
   note_kernel_t("encode_static_kernel", K, P);
   const unsigned g = stream_grid(a.ntasks);
-  RowArgs b = with_order(a, kOrderStaticEncode);
-  const hipError_t e = gate_rows(b, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, b);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, with_order(a, kOrderStaticEncode));
   return hipGetLastError();
 }
 
@@ -189,10 +183,7 @@ hipError_t launch_cauchy(const RowArgs& a, hipStream_t s) {
   auto kern = encode_cauchy_kernel<K, P>;
   note_kernel_t("encode_cauchy_kernel", K, P);
   const unsigned g = stream_grid(a.ntasks);
-  RowArgs b = with_order(a, kOrderStaticEncode);
-  const hipError_t e = gate_rows(b, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, b);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlockThreads), 0, s, with_order(a, kOrderStaticEncode));
   return hipGetLastError();
 }
 
@@ -226,8 +217,6 @@ template <int NINB>
 hipError_t launch_xor_n(const RowArgs& a, hipStream_t s) {
   auto kern = xor_kernel<NINB>;
   note_kernel_t("xor_kernel", NINB);
-  const hipError_t e = gate_other(s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks)), dim3(kBlockThreads), 0, s, with_order(a, kOrderStaticEncode));
   return hipGetLastError();
 }
@@ -243,8 +232,6 @@ hipError_t launch_xor(const RowArgs& a, hipStream_t s) {
 hipError_t launch_bytewise(const RowArgs& a, hipStream_t s) {
   const unsigned g = grid_for(bytewise_kernel, kBlockThreads, a.ntasks);
   note_kernel("bytewise_kernel");
-  const hipError_t e = gate_other(s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bytewise_kernel, dim3(g), dim3(kBlockThreads), 0, s, a);
   return hipGetLastError();
 }

@@ -104,54 +104,6 @@ struct GridCap {
   ~GridCap() { t_grid_cap = prev; }
 };
 
-// The queued host pipeline's gate context (hrs_hostpath.cpp queued_run), set
-// for the calling thread around the launches of one call. Launchers of the
-// gate-capable kernels (static encode, runtime-matrix resident / pipelined,
-// fused encode + CRC, fused repair + CRC) take the gate into their arguments
-// (gate_args) when the launch covers ONE stripe in windows that divide the
-// chunk; every other launch or queued operation first queues a gate kernel
-// that waits for the last chunk (gate_other), so any plan stays correct, only
-// without overlap. `gated` / `other` tell the host whether the done flags
-// cover the call.
-struct GateCtx {
-  Gate proto;            // ready, done, fail, timeout, tag (tpc, done_tag per launch)
-  uint64_t chunk_bytes;  // row bytes per chunk
-  uint32_t nchunks;
-  uint32_t next_done;    // done_tag of the next gated launch
-  uint32_t last_done = 0, last_tpc = 0;
-  int gated = 0;
-  int other = 0;
-};
-inline thread_local GateCtx* t_gate = nullptr;
-
-inline hipError_t gate_other(hipStream_t s) {
-  GateCtx* g = t_gate;
-  if (!g) return hipSuccess;
-  ++g->other;
-  return launch_gate(g->proto.ready, g->proto.tag + g->nchunks, g->proto.fail, g->proto.timeout, s);
-}
-
-// The gate of a gate-capable launch over `nstripes` stripes of windows of
-// `window_bytes` (or, when that launch cannot be gated, a gate_other first).
-inline hipError_t gate_args(Gate& out, uint64_t window_bytes, uint64_t nstripes, hipStream_t s) {
-  out = Gate{};
-  GateCtx* g = t_gate;
-  if (!g) return hipSuccess;
-  if (nstripes != 1 || window_bytes == 0 || g->chunk_bytes % window_bytes) return gate_other(s);
-  out = g->proto;
-  out.tpc = static_cast<uint32_t>(g->chunk_bytes / window_bytes);
-  out.done_tag = g->next_done++;
-  g->last_done = out.done_tag;
-  g->last_tpc = out.tpc;
-  ++g->gated;
-  return hipSuccess;
-}
-
-// A RowArgs launch of a gate-capable kernel: 2 KiB windows, ntasks / nwin stripes.
-inline hipError_t gate_rows(RowArgs& a, hipStream_t s) {
-  return gate_args(a.gate, kWindowBytes, a.nwin ? a.ntasks / a.nwin : 0, s);
-}
-
 inline unsigned capped_grid(uint64_t g) {
   if (t_grid_cap && g > t_grid_cap) g = t_grid_cap;
   return static_cast<unsigned>(g == 0 ? 1 : g);

@@ -17,11 +17,9 @@ template <int NOUT, int NINB>
 __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs a) {
   const int lane = threadIdx.x & 63;
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
-  uint32_t seen = a.gate.tag;  // queued host pipeline (gate_wait)
   for (uint32_t j = 0; j < 0xFFFFFFFFu; ++j) {
     const uint64_t t = wt.at(j);
     if (t >= wt.end) break;
-    if (!gate_wait(a.gate, t, seen)) return;
     int nin = a.nin;  // opaque per task: the r < nin predicates are not hoisted (they would spill)
     asm volatile("" : "+s"(nin));
     const uint64_t stripe = t / a.nwin;
@@ -53,7 +51,6 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_kernel(const RowArgs 
       bitslice(acc[o]);
       store_row(a.out[o] + stripe * a.out_stride + off, lane, acc[o]);
     }
-    gate_done(a.gate, t);
   }
 }
 
@@ -110,28 +107,18 @@ __global__ void __launch_bounds__(kBlockThreads) bitsliced_pipe_kernel(const Row
   asm volatile("" : "+s"(nin));
   const WaveTasks wt = wave_tasks(a.ntasks, a.order);
   uint32_t j = 0;
-  uint32_t seen = a.gate.tag;  // queued host pipeline: a task's chunk is waited for before its loads
   uint64_t t = wt.at(0);
   if (t >= wt.end) return;
   uint32_t ra[NINB][8], rb[NINB][8];
-  if (!gate_wait(a.gate, t, seen)) return;
   load_task<NOUT, NINB>(a, t, nin, lane, ra);
   for (;;) {  // every wave leaves once its next task index passes its end
     const uint64_t t1 = wt.at(++j);
-    if (t1 < wt.end) {
-      if (!gate_wait(a.gate, t1, seen)) return;
-      load_task<NOUT, NINB>(a, t1, nin, lane, rb);
-    }
+    if (t1 < wt.end) load_task<NOUT, NINB>(a, t1, nin, lane, rb);
     apply_task<NOUT, NINB>(a, t, nin, lane, ra);
-    gate_done(a.gate, t);
     if (t1 >= wt.end) break;
     const uint64_t t2 = wt.at(++j);
-    if (t2 < wt.end) {
-      if (!gate_wait(a.gate, t2, seen)) return;
-      load_task<NOUT, NINB>(a, t2, nin, lane, ra);
-    }
+    if (t2 < wt.end) load_task<NOUT, NINB>(a, t2, nin, lane, ra);
     apply_task<NOUT, NINB>(a, t1, nin, lane, rb);
-    gate_done(a.gate, t1);
     if (t2 >= wt.end) break;
     t = t2;
   }
@@ -238,10 +225,7 @@ hipError_t launch_bits_n(const RowArgs& a, hipStream_t s) {
     }
   note_kernel_t(name, NOUT, NINB);
   const int per_cu = BitLoop<NOUT, NINB>::kRolled ? 3 : 2;
-  RowArgs b = with_order(a, kOrderRuntime);
-  const hipError_t e = gate_rows(b, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, b);
+  hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderRuntime));
   return hipGetLastError();
 }
 
@@ -261,8 +245,6 @@ hipError_t launch_stream_n(const RowArgs& a, hipStream_t s) {
   auto kern = bitsliced_stream_kernel<NOUT, kStreamGroup>;
   note_kernel_t("bitsliced_stream_kernel", NOUT, kStreamGroup);
   const int per_cu = NOUT >= 4 ? 3 : 2;
-  const hipError_t e = gate_other(s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(stream_grid(a.ntasks, per_cu)), dim3(kBlockThreads), 0, s, with_order(a, kOrderRuntime));
   return hipGetLastError();
 }

@@ -24,7 +24,7 @@ def test_host_crc_exported():
     assert hasattr(L, "hrs_encode_crc") and hasattr(L, "hrs_decode_crc")
 
 
-@pytest.fixture(params=["zero_copy", "copy_engine", "gated", "queued"])
+@pytest.fixture(params=["zero_copy", "copy_engine", "gated"])
 def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
     bytes: the staged zero-copy path (the default: rows copied into pinned
@@ -32,12 +32,10 @@ def transfer_mode(request, monkeypatch):
     engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H), and the gated
     queue (HRS_HOST_GATE=1, 128 KiB chunks after a 64 KiB first one over 4
     slots: every chunk's kernels queued ahead behind gate kernels the host
-    opens after each copy-in), and the queued pipeline (HRS_HOST_QUEUE=1: one
-    launch per call whose waves wait for their 64 KiB chunk in the kernel). Which caller memory runs in place
+    opens after each copy-in). Which caller memory runs in place
     (runtime-pinned only) is test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
-    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST", "HRS_HOST_QUEUE",
-                "HRS_HOST_QCHUNK"):
+    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST"):
         monkeypatch.delenv(var, raising=False)
     if request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
@@ -47,12 +45,8 @@ def transfer_mode(request, monkeypatch):
         monkeypatch.setenv("HRS_HOST_CHUNK", "131072")
         monkeypatch.setenv("HRS_HOST_SLOTS", "4")
         monkeypatch.setenv("HRS_HOST_FIRST", "65536")
-    elif request.param == "queued":  # one launch gated per 64 KiB chunk in the kernel (queued_run)
-        monkeypatch.setenv("HRS_HOST_QUEUE", "1")
-        monkeypatch.setenv("HRS_HOST_QCHUNK", "65536")
     else:
         monkeypatch.setenv("HRS_HOST_GATE", "0")
-        monkeypatch.setenv("HRS_HOST_QUEUE", "0")
     return request.param
 
 

@@ -11,7 +11,7 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "gated", "queued"])
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "gated"])
 def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
     bytes: the staged zero-copy path (the default: rows copied into pinned
@@ -19,12 +19,10 @@ def transfer_mode(request, monkeypatch):
     engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H), and the gated
     queue (HRS_HOST_GATE=1, 128 KiB chunks after a 64 KiB first one over 4
     slots: every chunk's kernels queued ahead behind gate kernels the host
-    opens after each copy-in), and the queued pipeline (HRS_HOST_QUEUE=1: one
-    launch per call whose waves wait for their 64 KiB chunk in the kernel). Which caller memory runs in place
+    opens after each copy-in). Which caller memory runs in place
     (runtime-pinned only) is test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
-    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST", "HRS_HOST_QUEUE",
-                "HRS_HOST_QCHUNK"):
+    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST"):
         monkeypatch.delenv(var, raising=False)
     if request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
@@ -34,12 +32,8 @@ def transfer_mode(request, monkeypatch):
         monkeypatch.setenv("HRS_HOST_CHUNK", "131072")
         monkeypatch.setenv("HRS_HOST_SLOTS", "4")
         monkeypatch.setenv("HRS_HOST_FIRST", "65536")
-    elif request.param == "queued":  # one launch gated per 64 KiB chunk in the kernel (queued_run)
-        monkeypatch.setenv("HRS_HOST_QUEUE", "1")
-        monkeypatch.setenv("HRS_HOST_QCHUNK", "65536")
     else:
         monkeypatch.setenv("HRS_HOST_GATE", "0")
-        monkeypatch.setenv("HRS_HOST_QUEUE", "0")
     return request.param
 
 
@@ -115,14 +109,14 @@ def test_host_calls_on_pinned_rows(cuda, transfer_mode, L):
 
 
 def test_gate_miss_reruns_without_gates(cuda, transfer_mode, monkeypatch):
-    """A gate (gate kernel, or a queued kernel's wave) that gives up waiting (its host stalled past the timeout; test
+    """A gate kernel that gives up waiting (its host stalled past the timeout; test
     hooks HRS_GATE_TIMEOUT_US / HRS_GATE_DELAY_US) lets its chunk's kernels
     run on stale staging; the call must notice the miss, discard those
     results and run again without gates: bit-exact outputs and CRCs."""
     import time
     import zlib
-    if transfer_mode not in ("gated", "queued"):
-        pytest.skip("gated pipelines only")
+    if transfer_mode != "gated":
+        pytest.skip("gated pipeline only")
     k, p, L = 10, 4, 1 << 20
     code = HipReedSolomonCode(k, p, zero_inputs_after_encode=False)
     rng = np.random.default_rng(77)

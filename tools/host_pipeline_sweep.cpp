@@ -1,7 +1,7 @@
 // A/B sweep of the staged synchronous host-buffer pipeline's knobs
 // (hrs_hostpath.cpp staged_run: HRS_HOST_CHUNK, HRS_HOST_SLOTS,
-// HRS_HOST_FIRST, HRS_HOST_GATE, HRS_HOST_QUEUE / HRS_HOST_QCHUNK, all read
-// per call), interleaved round by
+// HRS_HOST_FIRST, HRS_HOST_GATE, HRS_HOST_NT, all read per call), interleaved
+// round by
 // round in one process over the four calls the JNI shim makes per Encoder /
 // Decoder round: hrs_encode / hrs_decode / hrs_encode_crc / hrs_decode_crc on
 // one RS(k,p) stripe of L-byte pageable rows (default RS(10,4), 1 MiB).
@@ -108,14 +108,8 @@ int main(int argc, char** argv) {
       setenv("HRS_HOST_CHUNK", V.chunk.c_str(), 1);
       setenv("HRS_HOST_SLOTS", V.slots.c_str(), 1);
       setenv("HRS_HOST_FIRST", V.first.c_str(), 1);
-      // gate 2 = the queued pipeline (one gated launch per call, HRS_HOST_QUEUE,
-      // chunk -> HRS_HOST_QCHUNK); 0 / 1 = the chunked pipeline without / with gate kernels
-      const bool queued = V.gate == "2";
-      setenv("HRS_HOST_QUEUE", queued ? "1" : "0", 1);
-      setenv("HRS_HOST_QCHUNK", V.chunk.c_str(), 1);
-      setenv("HRS_HOST_GATE", queued ? "0" : V.gate.c_str(), 1);
-      setenv("HRS_HOST_NT", queued ? "0" : V.nt.c_str(), 1);
-      setenv("HRS_HOST_QUC", queued ? V.nt.c_str() : "0", 1);  // queued: the nt field selects coherent staging
+      setenv("HRS_HOST_GATE", V.gate.c_str(), 1);
+      setenv("HRS_HOST_NT", V.nt.c_str(), 1);
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
