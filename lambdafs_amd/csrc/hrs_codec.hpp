@@ -81,6 +81,7 @@ struct hrs_codec {
   uint32_t qtag = 0;
   uint64_t gate_timeout = 0;
   std::set<uint64_t> staged_shapes;
+  std::map<uint64_t, std::vector<uint32_t>> crc_ztabs;  // Z_n as 4 x 256 tables, by n (host folds)
   // host-memory batches (hrs_*_batch_host): a ring of chunk slots, each a
   // device image + output block, pinned staging (pageable callers only) and
   // its own compute stream; every slot's H2D goes on one copy-in stream and
@@ -204,12 +205,17 @@ hrs_status run_apply(hrs_codec* c, const uint8_t* m, int nout, int nin, const ui
 size_t crc_raw_bytes_for(size_t len, size_t nstripes, int nrows);
 hrs_status run_crc(hrs_codec* c, const uint8_t* const* rows, const size_t* strides, int nrows, size_t len,
                    size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw);
+// host_fold_win != NULL: when the fused one-pass kernel runs, no fold is
+// launched; the raw window CRCs stay in `raw` (layout [stripe][row][window])
+// and *host_fold_win receives the window size for the caller's host fold
+// (0: the two-pass path ran and wrote crc_out itself).
 hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
                            size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
-                           hipStream_t s, uint32_t* raw);
+                           hipStream_t s, uint32_t* raw, uint64_t* host_fold_win = nullptr);
 hrs_status apply_crc_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                           size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
-                          const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw);
+                          const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw,
+                          uint64_t* host_fold_win = nullptr);
 // Whether encode_crc_impl / apply_crc_impl (nlive live inputs) take their
 // one-pass kernel for a job of this shape, rows 16-byte aligned: the
 // zero-copy host calls checksum through host memory only then (a two-pass CRC

@@ -435,7 +435,8 @@ bool apply_crc_one_pass(const hrs_codec* c, int nout, int nlive, size_t len) {
 
 hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t in_stride, uint8_t* const* out_rows,
                            size_t out_stride, size_t len, size_t nstripes, const uint32_t* crc_in, uint32_t* crc_out,
-                           hipStream_t s, uint32_t* raw) {
+                           hipStream_t s, uint32_t* raw, uint64_t* host_fold_win) {
+  if (host_fold_win) *host_fold_win = 0;
   const int k = c->k, p = c->p, n = c->n;
   // one pass: a static (k, p) of rs / nrs, whole 2 KiB sub-windows, 16-byte aligned rows.
   // A wave walks its window's sub-windows serially over k + p rows (~20 us
@@ -466,6 +467,10 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
     hipError_t e = hrs::launch_encode_crc(family, k, p, a, hrs::device_cu_count(), s, &handled);
     if (e != hipSuccess) return hip_fail(c, e, "fused encode+crc launch");
     if (handled) c->last_kernel = hrs::last_kernel();
+    if (handled && host_fold_win) {  // the caller folds the raw window CRCs on the host
+      *host_fold_win = subs * hrs::kWindowBytes;
+      return HRS_OK;
+    }
     if (handled) return crc_fold(c, len, nstripes * n, crc_in, crc_out, s, raw, subs * hrs::kWindowBytes);
   }
   // two passes: encode, then the CRC of the k sources and p parities
@@ -493,7 +498,9 @@ hrs_status encode_crc_impl(hrs_codec* c, const uint8_t* const* in_rows, size_t i
 // the apply, then the CRC pass over its outputs.
 hrs_status apply_crc_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, const uint8_t* const* in_rows,
                           size_t in_stride, uint8_t* const* out_rows, size_t out_stride, size_t len, size_t nstripes,
-                          const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw) {
+                          const uint32_t* crc_in, uint32_t* crc_out, hipStream_t s, uint32_t* raw,
+                          uint64_t* host_fold_win) {
+  if (host_fold_win) *host_fold_win = 0;
   if (nout < 0 || nin < 0 || nout > 255 || nin > 255) return fail(c, HRS_EINVAL, "bad matrix shape %dx%d", nout, nin);
   if (nout == 0 || nstripes == 0) return HRS_OK;
   for (int o = 0; o < nout; ++o)
@@ -533,6 +540,10 @@ hrs_status apply_crc_impl(hrs_codec* c, const uint8_t* m, int nout, int nin, con
     if (e != hipSuccess) return hip_fail(c, e, "fused decode+crc launch");
     if (handled) {
       c->last_kernel = hrs::last_kernel();
+      if (host_fold_win) {  // the caller folds the raw window CRCs on the host
+        *host_fold_win = hrs::kWindowBytes;
+        return HRS_OK;
+      }
       return crc_fold(c, len, nstripes * nout, crc_in, crc_out, s, raw, hrs::kWindowBytes);
     }
   }

@@ -72,6 +72,28 @@ const hrs::crc::Mat& crc_zmat(hrs_codec* c, uint64_t len) {
   return it->second;
 }
 
+// Z_len as 4 byte-indexed tables (crc32.hpp to_tables), for host folds.
+const uint32_t* crc_ztab(hrs_codec* c, uint64_t len) {
+  auto it = c->crc_ztabs.find(len);
+  if (it == c->crc_ztabs.end()) {
+    std::vector<uint32_t> t(4 * 256);
+    hrs::crc::to_tables(crc_zmat(c, len), t.data());
+    it = c->crc_ztabs.emplace(len, std::move(t)).first;
+  }
+  return it->second.data();
+}
+
+inline uint32_t ztab_apply(const uint32_t* t, uint32_t v) {
+  return t[v & 0xFFu] ^ t[256 + ((v >> 8) & 0xFFu)] ^ t[512 + ((v >> 16) & 0xFFu)] ^ t[768 + (v >> 24)];
+}
+
+// Checksummed staged chunks fold their raw window CRCs on the host
+// (HRS_HOST_FOLD=0: a fold kernel per chunk, the round-5 form; read per call).
+bool host_fold_on() {
+  const char* e = getenv("HRS_HOST_FOLD");
+  return !(e && e[0] == '0');
+}
+
 // Rows the caller holds in memory the runtime allocated pinned (hipHostMalloc,
 // torch pin_memory) are visible to the GPU at their own addresses and never
 // move: the zero-copy kernel runs over them in place, one launch, no staging
@@ -238,6 +260,8 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   // ncrc CRC words, then the raw window-CRC scratch (device side only)
   const size_t crc_off = pitch * static_cast<size_t>(nlive + nout);
   const size_t raw_off = crc_off + ((ncrc * sizeof(uint32_t) + 255) & ~static_cast<size_t>(255));
+  // raw window CRCs: in the device buffer for a fold kernel; for a host fold
+  // (zero-copy chunks) in the pinned staging at the same offset
   const size_t need = ncrc ? raw_off + crc_raw_bytes_for(chunk, 1, ncrc) : crc_off;
   for (int i = 0; i < S; ++i) {
     hrs_status st = host_slot(c, i, need);
@@ -284,10 +308,26 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     for (int i = 0; i < nin; ++i)
       if (slot_of[i] >= 0) jobs.push_back({h.pin + pitch * slot_of[i], in_rows[i] + ch[j].off, ch[j].len, nt});
   };
+  std::vector<uint64_t> fold_win(C, 0);  // window of a chunk whose raw CRCs the host folds (0: GPU-folded)
   auto copy_out = [&](size_t j) {
     const hrs_codec::HostSlot& h = c->host[j % S];
     for (int o = 0; o < nout; ++o) jobs.push_back({out_rows[o] + ch[j].off, h.pin + pitch * (nlive + o), ch[j].len});
-    if (ncrc) std::memcpy(&parts[j * ncrc], h.pin + crc_off, ncrc * sizeof(uint32_t));
+    if (!ncrc) return;
+    if (!fold_win[j]) {
+      std::memcpy(&parts[j * ncrc], h.pin + crc_off, ncrc * sizeof(uint32_t));
+      return;
+    }
+    // CRC-32 of the chunk's cell of row r from its raw window CRCs
+    // (crc32.hpp: raw(A || B) = Z_|B|(raw(A)) ^ raw(B); crc = Z_len(~0) ^ raw ^ ~0)
+    const size_t nw = ch[j].len / fold_win[j];
+    const uint32_t* zw = crc_ztab(c, fold_win[j]);
+    const uint32_t* zl = crc_ztab(c, ch[j].len);
+    const uint32_t* raw = reinterpret_cast<const uint32_t*>(h.pin + raw_off);
+    for (int r = 0; r < ncrc; ++r) {
+      uint32_t x = 0;
+      for (size_t w = 0; w < nw; ++w) x = ztab_apply(zw, x) ^ raw[r * nw + w];
+      parts[j * ncrc + r] = ztab_apply(zl, ~0u) ^ x ^ ~0u;
+    }
   };
   auto flush = [&] {
     if (!jobs.empty()) pool.run(jobs);
@@ -309,12 +349,16 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     for (int i = 0; i < nin; ++i) din[i] = slot_of[i] >= 0 ? img + pitch * slot_of[i] : nullptr;
     for (int o = 0; o < nout; ++o) dout[o] = img + pitch * (nlive + o);
     uint32_t* dcrc = reinterpret_cast<uint32_t*>(img + crc_off);
-    uint32_t* draw = reinterpret_cast<uint32_t*>(h.dev + raw_off);
+    // zero-copy chunks leave their raw window CRCs in the pinned staging and
+    // the host folds them at copy-out (no fold launch per chunk)
+    const bool hf = zc && host_fold_on();
+    uint32_t* draw = reinterpret_cast<uint32_t*>(hf ? h.pin_dev + raw_off : h.dev + raw_off);
+    uint64_t* fw = hf ? &fold_win[j] : nullptr;
     hrs_status st;
     if (crc.mode == kCrcEncode)
-      st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+      st = encode_crc_impl(c, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw, fw);
     else if (crc.mode == kCrcOutputs)  // repair + CRC of the repaired cells (fused where the shape allows)
-      st = apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw);
+      st = apply_crc_impl(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, nullptr, dcrc, h.stream, draw, fw);
     else
       st = run_apply(c, m, nout, nin, din.data(), 0, dout.data(), 0, lj, 1, h.stream, static_kp);
     if (st != HRS_OK) return st;

@@ -1,13 +1,13 @@
 // A/B sweep of the staged synchronous host-buffer pipeline's knobs
 // (hrs_hostpath.cpp staged_run: HRS_HOST_CHUNK, HRS_HOST_SLOTS,
-// HRS_HOST_FIRST, HRS_HOST_GATE, HRS_HOST_NT, all read per call), interleaved
+// HRS_HOST_FIRST, HRS_HOST_GATE, HRS_HOST_NT, HRS_HOST_FOLD, all read per call), interleaved
 // round by
 // round in one process over the four calls the JNI shim makes per Encoder /
 // Decoder round: hrs_encode / hrs_decode / hrs_encode_crc / hrs_decode_crc on
 // one RS(k,p) stripe of L-byte pageable rows (default RS(10,4), 1 MiB).
 // Every variant's parity, CRCs and repaired row must equal the first
 // variant's (and the repaired row the lost one), or the tool fails.
-// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate[:nt],...]
+// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate[:nt[:fold]],...]
 //   (one JSON line per variant, medians)
 #include <algorithm>
 #include <chrono>
@@ -21,7 +21,7 @@
 #include "../include/hrs.h"
 
 struct Variant {
-  std::string name, chunk, slots, first, gate, nt = "0";
+  std::string name, chunk, slots, first, gate, nt = "0", fold = "1";
 };
 
 // Default variants; argv[4] may list others as name:chunk:slots:first:gate,...
@@ -39,14 +39,14 @@ static std::vector<Variant> parse_variants(const char* spec) {
   while (pos < s.size()) {
     size_t end = s.find(',', pos);
     if (end == std::string::npos) end = s.size();
-    std::string item = s.substr(pos, end - pos), f[6] = {"", "", "", "", "", "0"};
+    std::string item = s.substr(pos, end - pos), f[7] = {"", "", "", "", "", "0", "1"};
     size_t q = 0;
-    for (int i = 0; i < 6 && q < item.size(); ++i) {
+    for (int i = 0; i < 7 && q < item.size(); ++i) {
       size_t c = item.find(':', q);
       f[i] = item.substr(q, c == std::string::npos ? std::string::npos : c - q);
       q = c == std::string::npos ? item.size() : c + 1;
     }
-    v.push_back({f[0], f[1], f[2], f[3], f[4], f[5]});
+    v.push_back({f[0], f[1], f[2], f[3], f[4], f[5], f[6]});
     pos = end + 1;
   }
   return v;
@@ -110,6 +110,7 @@ int main(int argc, char** argv) {
       setenv("HRS_HOST_FIRST", V.first.c_str(), 1);
       setenv("HRS_HOST_GATE", V.gate.c_str(), 1);
       setenv("HRS_HOST_NT", V.nt.c_str(), 1);
+      setenv("HRS_HOST_FOLD", V.fold.c_str(), 1);
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
