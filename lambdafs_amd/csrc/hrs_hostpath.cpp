@@ -183,16 +183,16 @@ static size_t env_window_bytes(const char* name, size_t dflt) {
 }
 
 // Defaults measured with tools/host_pipeline_sweep (profiles/r06/NOTES.md):
-// plain calls 256 KiB x 4 slots (RS(10,4) 1 MiB encode 0.280 ms against
-// 0.312 at 512 KiB x 2), checksummed calls 512 KiB x 2 (each chunk also
-// launches its CRC fold: fewer, larger chunks win there, 0.337 vs 0.348).
-size_t host_chunk_bytes(bool crc) { return env_window_bytes("HRS_HOST_CHUNK", (crc ? 512 : 256) << 10); }
+// 256 KiB x 4 slots. RS(10,4) 1 MiB calls, encode / decode / encode + CRC /
+// decode + CRC: 0.282 / 0.254 / 0.320 / 0.260 ms against 0.314 / 0.271 /
+// 0.348 / 0.271 at 512 KiB x 2 (the checksummed calls fold on the host).
+size_t host_chunk_bytes(bool) { return env_window_bytes("HRS_HOST_CHUNK", 256 << 10); }
 size_t host_first_bytes(size_t chunk) { return std::min(chunk, env_window_bytes("HRS_HOST_FIRST", chunk)); }
 
-int host_slots(bool crc) {
+int host_slots(bool) {
   const char* e = getenv("HRS_HOST_SLOTS");
   const int x = e ? atoi(e) : 0;
-  return (x >= 2 && x <= hrs::kHostSlots) ? x : (crc ? 2 : 4);
+  return (x >= 2 && x <= hrs::kHostSlots) ? x : 4;
 }
 
 // Copy-ins into the staging with nontemporal stores (HRS_HOST_NT, read per
