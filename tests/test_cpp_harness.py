@@ -111,18 +111,14 @@ def test_harness_decoder_restart_mid_block(cuda, args):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("direct", ["0", "1"])
 @pytest.mark.parametrize("threads", [2, 4])
-def test_harness_concurrent_handles(cuda, threads, direct):
+def test_harness_concurrent_handles(cuda, threads):
     """One codec per thread (Encoder.java:80, Decoder.java:90,
     MapReduceBlockRepairManager.java:426): threads interleave encodeBulk and
     decodeBulk (1-4 lost locations, changing every round) of RS(10,4) 1 MiB
-    cells on their own handles; every round bit-exact vs the oracle's parity
-    and the original cells. Staged (the default) and with the opt-in direct
-    path (HRS_HOST_DIRECT=1, overlapping calls allowed so the page claims
-    see shared rows)."""
-    env = {"HRS_HOST_DIRECT": direct, "HRS_HOST_DIRECT_EXCL": "0"}
-    rc, res = run(f"--threads={threads}", "--rounds=12", 10, 4, 1 << 20, 1 << 20, 1, 31, env=env)
+    cells on their own handles (pageable, so staged); every round bit-exact
+    vs the oracle's parity and the original cells."""
+    rc, res = run(f"--threads={threads}", "--rounds=12", 10, 4, 1 << 20, 1 << 20, 1, 31)
     assert rc == 0 and res["ok"], res
 
 

@@ -4,10 +4,11 @@ the JNI path of Encoder.encodeStripe with computeBlockChecksum
 parityChecksums over writeBufs) and of the Decoder's repaired-block check
 (Decoder.java:222-229, :645-655).
 
-Cells pass through the pinned-staging pipeline in 512 KiB column chunks; each
-chunk's CRCs are computed on the GPU next to the encode (fused kernel on
-32 KiB-multiple chunks, two passes on ragged ones) and chained on the host
-with zlib's crc32_combine operator. Parity and repaired rows are checked
+Cells pass through the pinned-staging pipeline in column chunks
+(HRS_HOST_CHUNK, default 256 KiB); each chunk's raw window CRCs are computed
+on the GPU next to the encode (fused kernel on 32 KiB-multiple chunks, two
+passes on ragged ones), folded on the host as the chunk is copied out
+(HRS_HOST_FOLD) and chained with zlib's crc32_combine operator. Parity and repaired rows are checked
 against the oracle, CRCs against zlib.crc32 (the JDK's java.util.zip.CRC32
 is zlib's CRC-32)."""
 import zlib

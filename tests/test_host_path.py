@@ -1,6 +1,6 @@
 """The synchronous host-buffer calls (hrs_encode / hrs_decode, the JNI path)
 through the pipelined pinned-staging host path: rows longer than one chunk
-(HRS_HOST_CHUNK, default 512 KiB), ragged last chunks, several calls in a row
+(HRS_HOST_CHUNK, default 256 KiB), ragged last chunks, several calls in a row
 (slot reuse), bit-exact against the oracle."""
 import numpy as np
 import pytest
