@@ -250,6 +250,12 @@ __global__ void __launch_bounds__(THREADS) encode_crc_grouped_kernel(const Encod
 
 // One 1024-thread block per CU (16 waves share the 156 KiB table image).
 constexpr int kFusedThreads = 1024;
+// Zero-copy jobs too small to give every CU of the grid 16 waves (a staged
+// host call's 256 KiB chunk: 128 windows, 8 blocks of 1,024) take 256-thread blocks
+// instead, still one per CU: 4x the CUs, so a wave's ~20 us of VALU work per
+// sub-window is shared by 1 wave per SIMD instead of 4 and the last window
+// finishes soon after its bytes arrive (HRS_FUSED_NARROW=0: always 1,024).
+constexpr int kFusedNarrowThreads = 256;
 
 // Rows per lockstep group, measured best (profiles/r02/sched): 2 (RS(10,4)
 // 3.10 ms vs 3.06-3.28 at 4), 4 from K = 12 (RS(12,4) 3.60 vs 3.72 at 2).
@@ -267,6 +273,11 @@ int fused_variant() {
     return 3;
   }();
   return v;
+}
+
+bool fused_narrow_on() {  // read per launch (A/B runs in one process)
+  const char* e = getenv("HRS_FUSED_NARROW");
+  return !(e && e[0] == '0');
 }
 
 int fused_group() {
@@ -292,10 +303,14 @@ template <int K, int P> constexpr const char* kMatrixName<gf::EncodeMatrix<K, P>
 template <int K, int P> constexpr const char* kMatrixName<gf::CauchyMatrix<K, P>> = "hrs::gf::CauchyMatrix";
 
 template <int K, int P, class MATRIX>
-CrcPick pick_kernel() {
+CrcPick pick_kernel(bool narrow) {
   constexpr const char* kg = "encode_crc_grouped_kernel";
   if (fused_variant() == 1) return {encode_crc_kernel<K, P, MATRIX, kFusedThreads>, kFusedThreads, "encode_crc_kernel", 0, -1};
   const int g = fused_group() ? fused_group() : kFusedGroup<K>;
+  if (fused_variant() == 3 && narrow && g == kFusedGroup<K>) {
+    constexpr int G = kFusedGroup<K> == 4 ? (K > 4 ? 4 : K) : 2;
+    return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedNarrowThreads, G, true>, kFusedNarrowThreads, kg, G, 1};
+  }
   if (fused_variant() == 3) {  // factored XOR network (xor_sched.hpp has G = 2, min(4, K), K)
     if (g == 4)
       return {encode_crc_grouped_kernel<K, P, MATRIX, kFusedThreads, (K > 4 ? 4 : K), true>, kFusedThreads, kg,
@@ -311,7 +326,12 @@ template <int K, int P, class MATRIX>
 hipError_t launch_one(const EncodeCrcArgs& a, int cus, hipStream_t s) {
   const size_t shm = static_cast<size_t>(kCrcLdsWordsA) * 4;
   const uint64_t ntasks = a.nstripes * a.nwin;
-  const CrcPick k = pick_kernel<K, P, MATRIX>();
+  // zero-copy launches only (a GridCap is set): device-resident jobs keep the
+  // 16 waves per CU that hide HBM latency
+  const uint64_t room = capped_grid(static_cast<uint64_t>(cus));  // blocks the grid may have
+  const bool narrow = t_grid_cap != 0 && fused_narrow_on() &&
+                      (ntasks + kFusedThreads / 64 - 1) / (kFusedThreads / 64) < room;
+  const CrcPick k = pick_kernel<K, P, MATRIX>(narrow);
   const std::string mat = std::string(kMatrixName<MATRIX>) + "<" + std::to_string(K) + ", " + std::to_string(P) + ">";
   if (k.sched < 0)
     note_kernel_t(k.base, K, P, mat.c_str(), k.threads);

@@ -7,7 +7,7 @@
 // one RS(k,p) stripe of L-byte pageable rows (default RS(10,4), 1 MiB).
 // Every variant's parity, CRCs and repaired row must equal the first
 // variant's (and the repaired row the lost one), or the tool fails.
-// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate[:nt[:fold]],...]
+// Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate[:nt[:fold[:K=V+K=V]]],...]
 //   (one JSON line per variant, medians)
 #include <algorithm>
 #include <chrono>
@@ -16,12 +16,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../include/hrs.h"
 
 struct Variant {
   std::string name, chunk, slots, first, gate, nt = "0", fold = "1";
+  std::string extra;  // more environment for this variant: KEY=VAL+KEY=VAL (unset for the others)
 };
 
 // Default variants; argv[4] may list others as name:chunk:slots:first:gate,...
@@ -39,17 +41,31 @@ static std::vector<Variant> parse_variants(const char* spec) {
   while (pos < s.size()) {
     size_t end = s.find(',', pos);
     if (end == std::string::npos) end = s.size();
-    std::string item = s.substr(pos, end - pos), f[7] = {"", "", "", "", "", "0", "1"};
+    std::string item = s.substr(pos, end - pos), f[8] = {"", "", "", "", "", "0", "1", ""};
     size_t q = 0;
-    for (int i = 0; i < 7 && q < item.size(); ++i) {
+    for (int i = 0; i < 8 && q < item.size(); ++i) {
       size_t c = item.find(':', q);
       f[i] = item.substr(q, c == std::string::npos ? std::string::npos : c - q);
       q = c == std::string::npos ? item.size() : c + 1;
     }
-    v.push_back({f[0], f[1], f[2], f[3], f[4], f[5], f[6]});
+    v.push_back({f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7]});
     pos = end + 1;
   }
   return v;
+}
+
+static std::vector<std::pair<std::string, std::string>> split_env(const std::string& s) {
+  std::vector<std::pair<std::string, std::string>> kv;
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find('+', pos);
+    if (end == std::string::npos) end = s.size();
+    const std::string item = s.substr(pos, end - pos);
+    const size_t eq = item.find('=');
+    if (eq != std::string::npos) kv.emplace_back(item.substr(0, eq), item.substr(eq + 1));
+    pos = end + 1;
+  }
+  return kv;
 }
 
 int main(int argc, char** argv) {
@@ -111,6 +127,9 @@ int main(int argc, char** argv) {
       setenv("HRS_HOST_GATE", V.gate.c_str(), 1);
       setenv("HRS_HOST_NT", V.nt.c_str(), 1);
       setenv("HRS_HOST_FOLD", V.fold.c_str(), 1);
+      for (const Variant& o : kVariants)  // other variants' extra keys unset, then this one's set
+        for (const auto& kv : split_env(o.extra)) unsetenv(kv.first.c_str());
+      for (const auto& kv : split_env(V.extra)) setenv(kv.first.c_str(), kv.second.c_str(), 1);
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
