@@ -32,7 +32,8 @@ tools/host_call_rate: tools/host_call_rate.cpp include/hrs.h $(LIB)
 
 # A/B of the staged pipeline's knobs, interleaved in one process (profiles/r06/).
 tools/host_pipeline_sweep: tools/host_pipeline_sweep.cpp include/hrs.h $(LIB)
-	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Llambdafs_amd -lhrs -Wl,-rpath,'$$ORIGIN/../lambdafs_amd'
+	g++ -O2 -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include -o $@ $< -Llambdafs_amd -lhrs \
+	    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../lambdafs_amd' -Wl,-rpath,/opt/rocm/lib
 
 # Host copy rates of the staging copies on the box's CPUs (profiles/r06/).
 tools/host_copy_probe: tools/host_copy_probe.cpp lambdafs_amd/csrc/hrs_host.hpp

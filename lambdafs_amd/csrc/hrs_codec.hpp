@@ -63,7 +63,7 @@ struct hrs_codec {
     bool pending = false;
   } batch[2];
   int batch_next = 0;
-  // host-buffer calls: chunk slots (4 by default, HRS_HOST_SLOTS 2-8),
+  // host-buffer calls: chunk slots (8 by default, HRS_HOST_SLOTS 2-8),
   // each pinned staging + device rows + its own stream; a slot is reused once
   // its D2H event has completed
   struct HostSlot {

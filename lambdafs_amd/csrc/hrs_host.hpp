@@ -11,7 +11,17 @@
 // the open batches in turn, each taking pieces of the batch it joined until
 // none is left (a piece per lock round trip cost a 5 MiB copy-in 40-80 us on
 // the MI355X hosts whatever the worker count: tools/pool_probe.cpp). A call
-// returns once all its pieces are copied and no worker still holds its batch.
+// returns once all its pieces are copied and no worker still holds its batch;
+// it spins for that (a condition-variable sleep at the end of every batch cost
+// about as much as the copy).
+//
+// Placement (round 6, tools/host_copy_probe): a host copy is bound by the CPU
+// complex (CCD) it runs on, about 70 GB/s each; threads on distinct CCDs add
+// up (4 threads copying a 2.5 MiB chunk: 188 GB/s on one L3, 271 GB/s over
+// four). So each worker is bound to the CPUs of its own L3 within the
+// process's affinity set, away from the constructing thread's L3, on its NUMA
+// node first (HRS_HOST_PIN=0: no binding). With an affinity set inside one L3
+// nothing is bound.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -22,11 +32,14 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
 #include <immintrin.h>
+#include <pthread.h>
 #include <sched.h>
 
 namespace hrs {
@@ -100,14 +113,21 @@ class CopyPool {
     }
     cv_.notify_all();
     drain(b);
-    // the last pieces are in other threads' hands: spin a while before
-    // sleeping (a condition-variable wake-up costs about a piece's copy)
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      close(&b);  // no new worker may join
+    }
+    // the last pieces are in other threads' hands: spin for them (held: as
+    // long as it takes; else a while) before sleeping
+    auto finished = [&] {
+      return b.done.load(std::memory_order_acquire) == b.pieces.size() && b.users.load(std::memory_order_acquire) == 0;
+    };
     const auto t0 = std::chrono::steady_clock::now();
-    while (b.done.load(std::memory_order_acquire) != b.pieces.size() && std::chrono::steady_clock::now() - t0 < kSpin)
-      __builtin_ia32_pause();
+    const bool held = holders_.load(std::memory_order_acquire) > 0;
+    while (!finished() && (held || std::chrono::steady_clock::now() - t0 < kSpin)) __builtin_ia32_pause();
+    if (finished()) return;
     std::unique_lock<std::mutex> lk(mu_);
-    close(&b);  // no new worker may join
-    done_cv_.wait(lk, [&] { return b.users == 0 && b.done.load() == b.pieces.size(); });
+    done_cv_.wait(lk, finished);
   }
 
   ~CopyPool() {
@@ -143,7 +163,7 @@ class CopyPool {
     std::vector<CopyJob> pieces;
     std::atomic<size_t> next{0};
     std::atomic<size_t> done{0};
-    int users = 0;  // workers inside drain(); guarded by mu_
+    std::atomic<int> users{0};  // workers inside drain(): raised under mu_ while the batch is open
   };
 
   // CPUs this process may run on: its affinity set, capped by a cgroup v2 CPU
@@ -166,12 +186,13 @@ class CopyPool {
 
   CopyPool() {
     const char* e = getenv("HRS_HOST_THREADS");
-    // default 2 workers (1 on a share under 4 CPUs): the caller plus two
-    // threads already reach what one CPU complex moves (the MI355X boxes give
-    // a job 16 CPUs of one CCD: ~77 GB/s copy on one thread, ~95-105 with the
-    // pool); more spinning workers only contend for it: RS(10,4) 1 MiB encode
-    // 0.280 ms with 2, 0.335 with 4, 0.37 with 8 (profiles/r06/NOTES.md)
-    int n = e ? atoi(e) : (cpu_share() >= 4 ? 2 : 1);
+    // default 3 workers (2 on a share under 8 CPUs, 1 under 4): with the
+    // caller, 4 threads copy a 1.25 MiB chunk at ~200 GB/s on the MI355X hosts
+    // (one thread ~75 GB/s); RS(10,4) 1 MiB staged encode 0.267 ms with 3,
+    // 0.274 with 2 (r06r). Each spins while a call holds the pool, so more
+    // only burn the job's CPU share (profiles/r06/NOTES.md).
+    const int share = cpu_share();
+    int n = e ? atoi(e) : (share >= 8 ? 3 : share >= 4 ? 2 : 1);
     if (n < 0) n = 0;
     if (n > 32) n = 32;
     nthreads_ = n;
@@ -180,7 +201,87 @@ class CopyPool {
     const char* pe = getenv("HRS_HOST_PIECE");
     const long pc = pe ? atol(pe) : 0;
     piece_ = pc >= 4096 ? static_cast<size_t>(pc) : static_cast<size_t>(256) << 10;
-    for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker(); });
+    const char* pin = getenv("HRS_HOST_PIN");
+    const std::vector<cpu_set_t> homes = (pin && pin[0] == '0') ? std::vector<cpu_set_t>() : worker_homes(n);
+    for (int i = 0; i < n; ++i) {
+      threads_.emplace_back([this] { worker(); });
+      if (!homes.empty())
+        (void)pthread_setaffinity_np(threads_.back().native_handle(), sizeof(cpu_set_t), &homes[i % homes.size()]);
+    }
+  }
+
+  // "0-7,128-135" -> CPU numbers
+  static std::vector<int> parse_cpulist(const char* text) {
+    std::vector<int> v;
+    const char* q = text;
+    while (*q) {
+      char* e = nullptr;
+      const long a = strtol(q, &e, 10);
+      if (e == q) break;
+      long b = a;
+      q = e;
+      if (*q == '-') {
+        b = strtol(q + 1, &e, 10);
+        q = e;
+      }
+      for (long x = a; x <= b; ++x) v.push_back(static_cast<int>(x));
+      while (*q == ',' || *q == '\n' || *q == ' ') ++q;
+    }
+    return v;
+  }
+
+  static int read_int(const std::string& path) {
+    int x = -1;
+    if (FILE* f = fopen(path.c_str(), "r")) {
+      if (fscanf(f, "%d", &x) != 1) x = -1;
+      fclose(f);
+    }
+    return x;
+  }
+
+  // One CPU set per worker: the allowed CPUs of one L3 each, the L3s on the
+  // constructing thread's NUMA node first, its own L3 last. Empty when the
+  // affinity set spans fewer than two L3s or sysfs says nothing.
+  static std::vector<cpu_set_t> worker_homes(int n) {
+    std::vector<cpu_set_t> homes;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (n <= 0 || sched_getaffinity(0, sizeof set, &set) != 0) return homes;
+    std::map<int, int> node_of;  // cpu -> NUMA node
+    for (int node = 0; node < 64; ++node) {
+      FILE* f = fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+      if (!f) continue;
+      char buf[4096] = {0};
+      const size_t got = fread(buf, 1, sizeof buf - 1, f);
+      fclose(f);
+      buf[got] = 0;
+      for (int cpu : parse_cpulist(buf)) node_of[cpu] = node;
+    }
+    std::map<int, std::vector<int>> l3;  // L3 id -> allowed CPUs
+    for (int cpu = 0; cpu < CPU_SETSIZE; ++cpu) {
+      if (!CPU_ISSET(cpu, &set)) continue;
+      const int id = read_int("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache/index3/id");
+      if (id < 0) return homes;
+      l3[id].push_back(cpu);
+    }
+    if (l3.size() < 2) return homes;
+    const int me = sched_getcpu();
+    const int my_l3 = me >= 0 ? read_int("/sys/devices/system/cpu/cpu" + std::to_string(me) + "/cache/index3/id") : -1;
+    const int my_node = node_of.count(me) ? node_of[me] : -1;
+    std::vector<std::pair<int, int>> order;  // (rank, L3 id): same node 0, other node 1, own L3 2
+    for (const auto& g : l3) {
+      const int node = node_of.count(g.second[0]) ? node_of[g.second[0]] : -1;
+      order.push_back({g.first == my_l3 ? 2 : node == my_node ? 0 : 1, g.first});
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
+    for (int i = 0; i < n && i < static_cast<int>(order.size()); ++i) {
+      cpu_set_t h;
+      CPU_ZERO(&h);
+      for (int cpu : l3[order[i].second]) CPU_SET(cpu, &h);
+      homes.push_back(h);
+    }
+    return homes;
   }
 
   // Copies pieces of b until none is left unclaimed.
@@ -226,13 +327,11 @@ class CopyPool {
           close(b);  // fully claimed: its caller finishes it
           continue;
         }
-        ++b->users;
+        b->users.fetch_add(1, std::memory_order_relaxed);
       }
       drain(*b);  // every piece left; one lock round trip per batch, not per piece
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        --b->users;
-      }
+      b->users.fetch_sub(1, std::memory_order_release);  // b may be gone after this
+      { std::lock_guard<std::mutex> lk(mu_); }            // a caller between its check and its wait is waiting now
       done_cv_.notify_all();
     }
   }

@@ -183,16 +183,19 @@ static size_t env_window_bytes(const char* name, size_t dflt) {
 }
 
 // Defaults measured with tools/host_pipeline_sweep (profiles/r06/NOTES.md):
-// 256 KiB x 4 slots. RS(10,4) 1 MiB calls, encode / decode / encode + CRC /
-// decode + CRC: 0.282 / 0.254 / 0.320 / 0.260 ms against 0.314 / 0.271 /
-// 0.348 / 0.271 at 512 KiB x 2 (the checksummed calls fold on the host).
-size_t host_chunk_bytes(bool) { return env_window_bytes("HRS_HOST_CHUNK", 256 << 10); }
+// 128 KiB x 8 slots, once the copy pool's batches stopped ending in a
+// condition-variable sleep (r06q / r06r, same box, 3 copy workers; RS(10,4)
+// 1 MiB calls, encode / decode / encode + CRC / decode + CRC): 0.267 / 0.245 /
+// 0.283 / 0.244 ms against 0.281 / 0.248 / 0.293 / 0.255 at 256 KiB x 4 (the
+// round-6 default before) and 0.314 / 0.271 / 0.348 / 0.271 at 512 KiB x 2
+// (round 5); in-place floor on pinned rows 0.224 / 0.213 / 0.238 / 0.221.
+size_t host_chunk_bytes(bool) { return env_window_bytes("HRS_HOST_CHUNK", 128 << 10); }
 size_t host_first_bytes(size_t chunk) { return std::min(chunk, env_window_bytes("HRS_HOST_FIRST", chunk)); }
 
 int host_slots(bool) {
   const char* e = getenv("HRS_HOST_SLOTS");
   const int x = e ? atoi(e) : 0;
-  return (x >= 2 && x <= hrs::kHostSlots) ? x : 4;
+  return (x >= 2 && x <= hrs::kHostSlots) ? x : 8;
 }
 
 // Copy-ins into the staging with nontemporal stores (HRS_HOST_NT, read per

@@ -5,7 +5,7 @@ parityChecksums over writeBufs) and of the Decoder's repaired-block check
 (Decoder.java:222-229, :645-655).
 
 Cells pass through the pinned-staging pipeline in column chunks
-(HRS_HOST_CHUNK, default 256 KiB); each chunk's raw window CRCs are computed
+(HRS_HOST_CHUNK, default 128 KiB over 8 slots); each chunk's raw window CRCs are computed
 on the GPU next to the encode (fused kernel on 32 KiB-multiple chunks, two
 passes on ragged ones), folded on the host as the chunk is copied out
 (HRS_HOST_FOLD) and chained with zlib's crc32_combine operator. Parity and repaired rows are checked
@@ -25,7 +25,7 @@ def test_host_crc_exported():
     assert hasattr(L, "hrs_encode_crc") and hasattr(L, "hrs_decode_crc")
 
 
-@pytest.fixture(params=["zero_copy", "copy_engine", "gated"])
+@pytest.fixture(params=["zero_copy", "copy_engine", "gated", "wide_chunks"])
 def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
     bytes: the staged zero-copy path (the default: rows copied into pinned
@@ -33,7 +33,8 @@ def transfer_mode(request, monkeypatch):
     engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H), and the gated
     queue (HRS_HOST_GATE=1, 128 KiB chunks after a 64 KiB first one over 4
     slots: every chunk's kernels queued ahead behind gate kernels the host
-    opens after each copy-in). Which caller memory runs in place
+    opens after each copy-in), and 512 KiB chunks over 2 slots (wide_chunks:
+    the 1,024-thread fused encode + CRC blocks). Which caller memory runs in place
     (runtime-pinned only) is test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
     for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST"):
@@ -46,6 +47,10 @@ def transfer_mode(request, monkeypatch):
         monkeypatch.setenv("HRS_HOST_CHUNK", "131072")
         monkeypatch.setenv("HRS_HOST_SLOTS", "4")
         monkeypatch.setenv("HRS_HOST_FIRST", "65536")
+    elif request.param == "wide_chunks":  # 512 KiB x 2 slots (round 5's default)
+        monkeypatch.setenv("HRS_HOST_GATE", "0")
+        monkeypatch.setenv("HRS_HOST_CHUNK", "524288")
+        monkeypatch.setenv("HRS_HOST_SLOTS", "2")
     else:
         monkeypatch.setenv("HRS_HOST_GATE", "0")
     return request.param

@@ -1,6 +1,6 @@
 """The synchronous host-buffer calls (hrs_encode / hrs_decode, the JNI path)
 through the pipelined pinned-staging host path: rows longer than one chunk
-(HRS_HOST_CHUNK, default 256 KiB), ragged last chunks, several calls in a row
+(HRS_HOST_CHUNK, default 128 KiB over 8 slots), ragged last chunks, several calls in a row
 (slot reuse), bit-exact against the oracle."""
 import numpy as np
 import pytest
@@ -11,7 +11,7 @@ from oracle import rs_oracle as C
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "gated"])
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_engine", "gated", "wide_chunks"])
 def transfer_mode(request, monkeypatch):
     """Every test runs each way the synchronous host-buffer calls can move
     bytes: the staged zero-copy path (the default: rows copied into pinned
@@ -19,7 +19,8 @@ def transfer_mode(request, monkeypatch):
     engine (HRS_ZEROCOPY=0: pinned staging, H2D, kernel, D2H), and the gated
     queue (HRS_HOST_GATE=1, 128 KiB chunks after a 64 KiB first one over 4
     slots: every chunk's kernels queued ahead behind gate kernels the host
-    opens after each copy-in). Which caller memory runs in place
+    opens after each copy-in), and 512 KiB chunks over 2 slots (wide_chunks:
+    the 1,024-thread fused encode + CRC blocks). Which caller memory runs in place
     (runtime-pinned only) is test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
     for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST"):
@@ -32,6 +33,10 @@ def transfer_mode(request, monkeypatch):
         monkeypatch.setenv("HRS_HOST_CHUNK", "131072")
         monkeypatch.setenv("HRS_HOST_SLOTS", "4")
         monkeypatch.setenv("HRS_HOST_FIRST", "65536")
+    elif request.param == "wide_chunks":  # 512 KiB x 2 slots (round 5's default)
+        monkeypatch.setenv("HRS_HOST_GATE", "0")
+        monkeypatch.setenv("HRS_HOST_CHUNK", "524288")
+        monkeypatch.setenv("HRS_HOST_SLOTS", "2")
     else:
         monkeypatch.setenv("HRS_HOST_GATE", "0")
     return request.param

@@ -7,6 +7,8 @@
 // one RS(k,p) stripe of L-byte pageable rows (default RS(10,4), 1 MiB).
 // Every variant's parity, CRCs and repaired row must equal the first
 // variant's (and the repaired row the lost one), or the tool fails.
+// ROWS=pinned in a variant's environment runs it on a hipHostMalloc'd copy of
+// the rows (the in-place path).
 // Usage: host_pipeline_sweep [calls] [rounds] [L] [name:chunk:slots:first:gate[:nt[:fold[:K=V+K=V]]],...]
 //   (one JSON line per variant, medians)
 #include <algorithm>
@@ -18,6 +20,8 @@
 #include <string>
 #include <utility>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "../include/hrs.h"
 
@@ -87,12 +91,15 @@ int main(int argc, char** argv) {
       z ^= z << 13, z ^= z >> 7, z ^= z << 17;
       memcpy(&rows[r][i], &z, 8);
     }
-  std::vector<const uint8_t*> in(k);
-  std::vector<uint8_t*> par(p);
-  for (int i = 0; i < k; ++i) in[i] = rows[p + i].data();
-  for (int r = 0; r < p; ++r) par[r] = rows[r].data();
   std::vector<uint8_t> lost(L);
-  uint8_t* lostp = lost.data();
+  // Row sets: the pageable rows above, and (variants with ROWS=pinned) a
+  // copy in hipHostMalloc'd memory, the in-place "pinned" path's floor.
+  struct RowSet {
+    std::vector<uint8_t*> row;
+    uint8_t* lost;
+  };
+  RowSet pageable{{}, lost.data()}, pinned{{}, nullptr};
+  for (int r = 0; r < n; ++r) pageable.row.push_back(rows[r].data());
   const int erased[1] = {p};
   int to_read[16];
   if (hrs_locations_to_read(c, erased, 1, to_read) != HRS_OK) return 1;
@@ -121,6 +128,26 @@ int main(int argc, char** argv) {
   for (int rd = 0; rd < rounds; ++rd)
     for (int v = 0; v < nv; ++v) {
       const Variant& V = kVariants[v];
+      bool use_pinned = false;
+      for (const auto& kv : split_env(V.extra)) use_pinned |= kv.first == "ROWS" && kv.second == "pinned";
+      if (use_pinned && pinned.row.empty()) {
+        void* m = nullptr;
+        if (hipHostMalloc(&m, (n + 1) * L, hipHostMallocDefault) != hipSuccess) {
+          fprintf(stderr, "hipHostMalloc failed\n");
+          return 1;
+        }
+        for (int r = 0; r < n; ++r) {
+          pinned.row.push_back(static_cast<uint8_t*>(m) + r * L);
+          memcpy(pinned.row[r], rows[r].data(), L);
+        }
+        pinned.lost = static_cast<uint8_t*>(m) + n * L;
+      }
+      const RowSet& rs = use_pinned ? pinned : pageable;
+      std::vector<const uint8_t*> in(k);
+      std::vector<uint8_t*> par(p);
+      for (int i = 0; i < k; ++i) in[i] = rs.row[p + i];
+      for (int r = 0; r < p; ++r) par[r] = rs.row[r];
+      uint8_t* lostp = rs.lost;
       setenv("HRS_HOST_CHUNK", V.chunk.c_str(), 1);
       setenv("HRS_HOST_SLOTS", V.slots.c_str(), 1);
       setenv("HRS_HOST_FIRST", V.first.c_str(), 1);
@@ -128,8 +155,10 @@ int main(int argc, char** argv) {
       setenv("HRS_HOST_NT", V.nt.c_str(), 1);
       setenv("HRS_HOST_FOLD", V.fold.c_str(), 1);
       for (const Variant& o : kVariants)  // other variants' extra keys unset, then this one's set
-        for (const auto& kv : split_env(o.extra)) unsetenv(kv.first.c_str());
-      for (const auto& kv : split_env(V.extra)) setenv(kv.first.c_str(), kv.second.c_str(), 1);
+        for (const auto& kv : split_env(o.extra))
+          if (kv.first != "ROWS") unsetenv(kv.first.c_str());
+      for (const auto& kv : split_env(V.extra))
+        if (kv.first != "ROWS") setenv(kv.first.c_str(), kv.second.c_str(), 1);
       for (int r = 0; r < p; ++r) memset(par[r], 0, L);
       t[v * 4 + 0].push_back(time_it([&] { ok &= hrs_encode(c, in.data(), par.data(), L) == HRS_OK; }));
       paths[v] = hrs_last_host_path(c);
@@ -140,13 +169,13 @@ int main(int argc, char** argv) {
         fprintf(stderr, "%s: parity differs from %s\n", V.name.c_str(), kVariants[0].name.c_str());
         ok = false;
       }
-      for (int i = 0; i < nr; ++i) reads[to_read[i]] = rows[to_read[i]].data();
+      for (int i = 0; i < nr; ++i) reads[to_read[i]] = rs.row[to_read[i]];
       memset(lostp, 0, L);
       t[v * 4 + 1].push_back(time_it([&] {
         ok &= hrs_decode(c, reads.data(), &lostp, erased, 1, to_read, nr, ntr.data(), static_cast<int>(ntr.size()),
                          L) == HRS_OK;
       }));
-      if (memcmp(lost.data(), rows[p].data(), L) != 0) {
+      if (memcmp(lostp, rs.row[p], L) != 0) {
         fprintf(stderr, "%s: repaired row differs\n", V.name.c_str());
         ok = false;
       }
@@ -163,7 +192,7 @@ int main(int argc, char** argv) {
                              static_cast<int>(ntr.size()), L, nullptr, dcrc.data()) == HRS_OK;
       }));
       if (rd == 0 && v == 0) ref_dcrc = dcrc[0];
-      if (dcrc[0] != ref_dcrc || memcmp(lost.data(), rows[p].data(), L) != 0) {
+      if (dcrc[0] != ref_dcrc || memcmp(lostp, rs.row[p], L) != 0) {
         fprintf(stderr, "%s: decode CRC or repaired row differs\n", V.name.c_str());
         ok = false;
       }
