@@ -397,7 +397,8 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
     if (st != HRS_OK) return st;
   }
   hrs::GridCap cap(zc ? zero_copy_blocks() : 0u);
-  hrs::CopyPool& pool = hrs::CopyPool::instance();
+  hrs::CopyPool& pool = copy_pool(c);
+  const uint8_t nt = host_store_mode();
   std::vector<hrs::CopyJob> jobs;
   const bool duplex = hbatch_duplex();
   struct Pending {
@@ -437,7 +438,7 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
         for (const RowRun& r : reads(s0 + i))
           for (int q = 0; q < r.cnt; ++q) {
             const int l = r.l0 + q;
-            jobs.push_back({h.pin + i * img_stripe + l * dpitch, hin + (s0 + i) * in_stripe + l * in_row, len});
+            jobs.push_back({h.pin + i * img_stripe + l * dpitch, hin + (s0 + i) * in_stripe + l * in_row, len, nt});
           }
       pool.run(jobs);
     }

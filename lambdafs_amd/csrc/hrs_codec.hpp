@@ -15,6 +15,10 @@
 #include "crc32.hpp"
 #include "hrs_internal.hpp"
 
+namespace hrs {
+class CopyPool;  // hrs_host.hpp
+}
+
 struct hrs_codec {
   int kind = HRS_CODE_RS;
   int k = 0;
@@ -125,6 +129,7 @@ struct hrs_codec {
   std::string err;
   std::string last_kernel;  // main kernel of the latest coding call (hrs_last_kernel)
   const char* last_host_path = "";  // hrs_last_host_path: "pinned" | "staged" | "copy_engine"
+  int numa_node = -2;               // NUMA node of the device's PCI function (-1 unknown, -2 not read yet)
 };
 
 
@@ -173,6 +178,12 @@ bool runtime_pinned(const void* p, size_t len);
 // Device address of runtime-pinned host memory [p, p + len) when it equals
 // the host address, or false (pageable or registered memory: staged).
 bool host_device_ptr(const void* p, size_t len, uint8_t** dp);
+// The host copy pool (hrs_host.hpp), its workers placed for this handle's
+// GPU: on the GPU's NUMA node, where its pinned staging lives, unless
+// HRS_HOST_HOME=caller (hrs_hostpath.cpp).
+hrs::CopyPool& copy_pool(hrs_codec* c);
+// How copy-ins store into pinned staging (hrs::kStore*; HRS_HOST_NT).
+uint8_t host_store_mode();
 
 // The compile-time encode kernels hold the hops RS generator (rs) or the
 // ISA-L Cauchy rows (nrs) of a (k, p) shape; only those families' G may take

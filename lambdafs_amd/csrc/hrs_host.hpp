@@ -44,12 +44,32 @@
 
 namespace hrs {
 
+// CopyJob::stream: how the destination lines are stored
+enum : uint8_t {
+  kStorePlain = 0,   // through this CPU's caches
+  kStoreStream = 1,  // nontemporal: dst is read next by a device, not by this CPU
+  kStoreRemote = 2,  // nontemporal only from a CPU off the pool's home NUMA node
+};
+
 struct CopyJob {
   void* dst;
   const void* src;
   size_t bytes;
-  bool stream = false;  // nontemporal stores: dst is read next by a device, not by this CPU
+  uint8_t stream = kStorePlain;
 };
+
+// The NUMA node the copy pool works for: the node of the GPU whose pinned
+// staging it fills (set by the library before the pool's first use; -1 none).
+inline std::atomic<int>& pool_home_node() {
+  static std::atomic<int> node{-1};
+  return node;
+}
+
+// NUMA node of the CPU the calling thread runs on, -1 if unknown.
+inline int current_node() {
+  unsigned cpu = 0, node = 0;
+  return getcpu(&cpu, &node) == 0 ? static_cast<int>(node) : -1;
+}
 
 // memcpy with nontemporal (streaming) stores: the destination lines go to
 // memory instead of this CPU's caches, so a device reading them next across
@@ -78,8 +98,13 @@ __attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const u
   _mm_sfence();  // the streamed lines are in memory before this copy counts as done
 }
 
-inline void copy_job(void* d, const void* s, size_t n, bool stream) {
+inline void copy_job(void* d, const void* s, size_t n, uint8_t mode) {
   static const bool avx2 = __builtin_cpu_supports("avx2");
+  bool stream = mode == kStoreStream;
+  if (mode == kStoreRemote) {
+    const int home = pool_home_node().load(std::memory_order_relaxed);
+    stream = home >= 0 && current_node() != home;
+  }
   if (stream && avx2)
     stream_copy_avx2(static_cast<uint8_t*>(d), static_cast<const uint8_t*>(s), n);
   else
@@ -91,6 +116,13 @@ class CopyPool {
   static CopyPool& instance() {
     static CopyPool pool;
     return pool;
+  }
+
+  // The GPU's NUMA node, for the workers' placement (first caller wins; call
+  // before the pool's first use for it to count).
+  static void set_home_node(int node) {
+    int none = -1;
+    if (node >= 0) pool_home_node().compare_exchange_strong(none, node);
   }
 
   void run(const std::vector<CopyJob>& jobs) {
@@ -240,8 +272,10 @@ class CopyPool {
   }
 
   // One CPU set per worker: the allowed CPUs of one L3 each, the L3s on the
-  // constructing thread's NUMA node first, its own L3 last. Empty when the
-  // affinity set spans fewer than two L3s or sysfs says nothing.
+  // home NUMA node first (the GPU's, set_home_node; HRS_HOST_HOME=caller or no
+  // home: the constructing thread's node), the constructing thread's own L3
+  // last. Empty when the affinity set spans fewer than two L3s or sysfs says
+  // nothing.
   static std::vector<cpu_set_t> worker_homes(int n) {
     std::vector<cpu_set_t> homes;
     cpu_set_t set;
@@ -267,11 +301,13 @@ class CopyPool {
     if (l3.size() < 2) return homes;
     const int me = sched_getcpu();
     const int my_l3 = me >= 0 ? read_int("/sys/devices/system/cpu/cpu" + std::to_string(me) + "/cache/index3/id") : -1;
-    const int my_node = node_of.count(me) ? node_of[me] : -1;
-    std::vector<std::pair<int, int>> order;  // (rank, L3 id): same node 0, other node 1, own L3 2
+    const char* he = getenv("HRS_HOST_HOME");
+    const int home = pool_home_node().load();
+    const int want_node = (home >= 0 && !(he && strcmp(he, "caller") == 0)) ? home : node_of.count(me) ? node_of[me] : -1;
+    std::vector<std::pair<int, int>> order;  // (rank, L3 id): wanted node 0, other node 1, own L3 2
     for (const auto& g : l3) {
       const int node = node_of.count(g.second[0]) ? node_of[g.second[0]] : -1;
-      order.push_back({g.first == my_l3 ? 2 : node == my_node ? 0 : 1, g.first});
+      order.push_back({g.first == my_l3 ? 2 : node == want_node ? 0 : 1, g.first});
     }
     std::stable_sort(order.begin(), order.end(),
                      [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });

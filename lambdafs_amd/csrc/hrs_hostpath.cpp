@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -198,11 +199,43 @@ int host_slots(bool) {
   return (x >= 2 && x <= hrs::kHostSlots) ? x : 8;
 }
 
-// Copy-ins into the staging with nontemporal stores (HRS_HOST_NT, read per
-// call): the GPU reads the staging next, across the link.
-bool host_stream_copies() {
+// Stores of the copy-ins into the pinned staging (HRS_HOST_NT, read per
+// call). The GPU reads the staging next, across the link, and the staging
+// lives on the GPU's NUMA node: lines a CPU of the other socket left dirty in
+// its caches make every such read a cross-socket snoop. Default ("auto"):
+// nontemporal stores from CPUs off the GPU's node, cached stores on it (RS(10,4)
+// 1 MiB staged encode from the other socket 0.339-0.359 ms with cached
+// stores, 0.273-0.284 with nontemporal; on the GPU's node 0.26 either way:
+// profiles/r06/NOTES.md, r06x). "1": always nontemporal, "0": never.
+uint8_t host_store_mode() {
   const char* e = getenv("HRS_HOST_NT");
-  return e && e[0] == '1';
+  if (!e || strcmp(e, "auto") == 0) return hrs::kStoreRemote;
+  return e[0] == '1' ? hrs::kStoreStream : hrs::kStorePlain;
+}
+
+// NUMA node of the handle's device: its PCI function's, from sysfs (cached).
+static int device_numa_node(hrs_codec* c) {
+  if (c->numa_node != -2) return c->numa_node;
+  int node = -1;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, c->device) == hipSuccess) {
+    for (char* q = bus; *q; ++q) *q = static_cast<char>(tolower(*q));
+    char path[160];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (FILE* f = fopen(path, "r")) {
+      if (fscanf(f, "%d", &node) != 1) node = -1;
+      fclose(f);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  c->numa_node = node;
+  return node;
+}
+
+hrs::CopyPool& copy_pool(hrs_codec* c) {
+  hrs::CopyPool::set_home_node(device_numa_node(c));
+  return hrs::CopyPool::instance();
 }
 
 bool host_gate_on() {
@@ -295,7 +328,7 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   }
   gate = gate && all_zc && seen && gate_flags(c);
   c->last_host_path = all_zc ? "staged" : "copy_engine";
-  hrs::CopyPool& pool = hrs::CopyPool::instance();
+  hrs::CopyPool& pool = copy_pool(c);
   std::vector<hrs::CopyJob> jobs;
   std::vector<uint32_t> parts(static_cast<size_t>(ncrc) * C);
   std::vector<const uint8_t*> din(nin);
@@ -305,7 +338,7 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
   // that is done (copy_out) and the next chunk's inputs (copy_in). A chunk's
   // input rows and output rows are disjoint regions of its slot, so a chunk's
   // copy-out and its slot's next copy-in may share a batch.
-  const bool nt = host_stream_copies();
+  const uint8_t nt = host_store_mode();
   auto copy_in = [&](size_t j) {
     const hrs_codec::HostSlot& h = c->host[j % S];
     for (int i = 0; i < nin; ++i)
@@ -573,8 +606,8 @@ hrs_status async_submit_impl(hrs_codec* c, hrs_codec::AsyncSlot& a, const uint8_
   if (st != HRS_OK) return st;
   std::vector<hrs::CopyJob> jobs;
   for (int i = 0; i < nin; ++i)
-    if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len});
-  hrs::CopyPool::instance().run(jobs);
+    if (slot_of[i] >= 0) jobs.push_back({a.pin + pitch * slot_of[i], in_rows[i], len, host_store_mode()});
+  copy_pool(c).run(jobs);
   uint8_t* const zpin = a.pin_dev;  // zero copy, as host_apply_impl
   const bool zc = zero_copy_on() && zpin &&
                   (crc_mode == kCrcEncode  ? encode_crc_one_pass(c, len, 1)
@@ -793,7 +826,7 @@ hrs_status hrs_collect(hrs_codec* c, uint64_t ticket, uint8_t* const* outputs, u
   if (st == HRS_OK && a->queued) {
     std::vector<hrs::CopyJob> jobs;
     for (int o = 0; o < a->nout; ++o) jobs.push_back({outputs[o], a->pin + a->pitch * (a->nlive + o), a->len});
-    hrs::CopyPool::instance().run(jobs);
+    copy_pool(c).run(jobs);
   }
   if (st == HRS_OK && a->ncrc > 0 && a->queued) {  // CRC32.update chaining: crc = Z_len(crc) ^ crc(cell)
     const uint32_t* part = reinterpret_cast<const uint32_t*>(a->pin + a->crc_off);

@@ -20,14 +20,18 @@ def transfer_mode(request, monkeypatch):
     queue (HRS_HOST_GATE=1, 128 KiB chunks after a 64 KiB first one over 4
     slots: every chunk's kernels queued ahead behind gate kernels the host
     opens after each copy-in), and 512 KiB chunks over 2 slots (wide_chunks:
-    the 1,024-thread fused encode + CRC blocks). Which caller memory runs in place
-    (runtime-pinned only) is test_host_memory.py."""
+    the 1,024-thread fused encode + CRC blocks). Copy-in stores: the default
+    (HRS_HOST_NT=auto, nontemporal off the GPU's NUMA node) for zero_copy and
+    gated, always nontemporal for wide_chunks, always cached for copy_engine.
+    Which caller memory runs in place (runtime-pinned only) is
+    test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
-    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST"):
+    for var in ("HRS_HOST_GATE", "HRS_HOST_CHUNK", "HRS_HOST_SLOTS", "HRS_HOST_FIRST", "HRS_HOST_NT"):
         monkeypatch.delenv(var, raising=False)
     if request.param == "copy_engine":
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
         monkeypatch.setenv("HRS_HOST_GATE", "0")
+        monkeypatch.setenv("HRS_HOST_NT", "0")
     elif request.param == "gated":  # gated queued chunks, small and many (hrs_hostpath.cpp staged_run)
         monkeypatch.setenv("HRS_HOST_GATE", "1")
         monkeypatch.setenv("HRS_HOST_CHUNK", "131072")
@@ -37,6 +41,7 @@ def transfer_mode(request, monkeypatch):
         monkeypatch.setenv("HRS_HOST_GATE", "0")
         monkeypatch.setenv("HRS_HOST_CHUNK", "524288")
         monkeypatch.setenv("HRS_HOST_SLOTS", "2")
+        monkeypatch.setenv("HRS_HOST_NT", "1")
     else:
         monkeypatch.setenv("HRS_HOST_GATE", "0")
     return request.param

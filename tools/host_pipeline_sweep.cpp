@@ -202,7 +202,7 @@ int main(int argc, char** argv) {
     return v[v.size() / 2];
   };
   for (int v = 0; v < nv; ++v)
-    printf("{\"variant\": \"%s\", \"chunk\": %s, \"slots\": %s, \"first\": %s, \"gate\": %s, \"nt\": %s, \"path\": \"%s\", "
+    printf("{\"variant\": \"%s\", \"chunk\": %s, \"slots\": %s, \"first\": %s, \"gate\": %s, \"nt\": \"%s\", \"path\": \"%s\", "
            "\"L\": %zu, \"calls\": %d, \"rounds\": %d, \"encode_ms\": %.4f, \"decode_ms\": %.4f, \"encode_crc_ms\": %.4f, "
            "\"decode_crc_ms\": %.4f, \"ok\": %s}\n",
            kVariants[v].name.c_str(), kVariants[v].chunk.c_str(), kVariants[v].slots.c_str(), kVariants[v].first.c_str(),
