@@ -202,15 +202,17 @@ int host_slots(bool) {
 // Stores of the copy-ins into the pinned staging (HRS_HOST_NT, read per
 // call). The GPU reads the staging next, across the link, and the staging
 // lives on the GPU's NUMA node: lines a CPU of the other socket left dirty in
-// its caches make every such read a cross-socket snoop. Default ("auto"):
-// nontemporal stores from CPUs off the GPU's node, cached stores on it (RS(10,4)
-// 1 MiB staged encode from the other socket 0.339-0.359 ms with cached
-// stores, 0.273-0.284 with nontemporal; on the GPU's node 0.26 either way:
-// profiles/r06/NOTES.md, r06x). "1": always nontemporal, "0": never.
+// its caches make every such read a cross-socket snoop. Default ("1"):
+// nontemporal stores, so the lines are in memory (RS(10,4) 1 MiB staged
+// encode from the other socket 0.33-0.36 ms with cached stores, 0.28 with
+// nontemporal; from the GPU's node 0.255-0.262 vs 0.264-0.269: never worse;
+// profiles/r06/NOTES.md §4, r06x / r06y). "auto": nontemporal only from CPUs
+// off the GPU's node; "0": cached.
 uint8_t host_store_mode() {
   const char* e = getenv("HRS_HOST_NT");
-  if (!e || strcmp(e, "auto") == 0) return hrs::kStoreRemote;
-  return e[0] == '1' ? hrs::kStoreStream : hrs::kStorePlain;
+  if (!e) return hrs::kStoreStream;
+  if (strcmp(e, "auto") == 0) return hrs::kStoreRemote;
+  return e[0] == '0' ? hrs::kStorePlain : hrs::kStoreStream;
 }
 
 // NUMA node of the handle's device: its PCI function's, from sysfs (cached).

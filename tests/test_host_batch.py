@@ -29,16 +29,16 @@ def transfer_mode(request, monkeypatch):
     kernel, D2H on each slot's stream), and the copy engine with the
     directions split over the shared copy-in / copy-out streams
     (HRS_HBATCH_DUPLEX=1: in_done / comp_done / done events chain the three
-    streams per slot). Staging copy-ins: the default stores (HRS_HOST_NT=auto)
-    for zero copy, always nontemporal for the copy engine, always cached for
-    duplex."""
+    streams per slot). Staging copy-ins: the default (nontemporal) stores for
+    zero copy, nontemporal only off the GPU's NUMA node (HRS_HOST_NT=auto) for
+    the copy engine, cached (0) for duplex."""
     monkeypatch.delenv("HRS_HBATCH_DUPLEX", raising=False)
     monkeypatch.delenv("HRS_HOST_NT", raising=False)
     if request.param == "zero_copy":
         monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
     else:
         monkeypatch.setenv("HRS_ZEROCOPY", "0")
-        monkeypatch.setenv("HRS_HOST_NT", "1")
+        monkeypatch.setenv("HRS_HOST_NT", "auto")
         if request.param == "duplex":
             monkeypatch.setenv("HRS_HBATCH_DUPLEX", "1")
             monkeypatch.setenv("HRS_HOST_NT", "0")

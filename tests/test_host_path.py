@@ -21,8 +21,8 @@ def transfer_mode(request, monkeypatch):
     slots: every chunk's kernels queued ahead behind gate kernels the host
     opens after each copy-in), and 512 KiB chunks over 2 slots (wide_chunks:
     the 1,024-thread fused encode + CRC blocks). Copy-in stores: the default
-    (HRS_HOST_NT=auto, nontemporal off the GPU's NUMA node) for zero_copy and
-    gated, always nontemporal for wide_chunks, always cached for copy_engine.
+    (nontemporal) for zero_copy and gated, nontemporal only off the GPU's NUMA
+    node (HRS_HOST_NT=auto) for wide_chunks, cached (0) for copy_engine.
     Which caller memory runs in place (runtime-pinned only) is
     test_host_memory.py."""
     monkeypatch.delenv("HRS_ZEROCOPY", raising=False)
@@ -41,7 +41,7 @@ def transfer_mode(request, monkeypatch):
         monkeypatch.setenv("HRS_HOST_GATE", "0")
         monkeypatch.setenv("HRS_HOST_CHUNK", "524288")
         monkeypatch.setenv("HRS_HOST_SLOTS", "2")
-        monkeypatch.setenv("HRS_HOST_NT", "1")
+        monkeypatch.setenv("HRS_HOST_NT", "auto")
     else:
         monkeypatch.setenv("HRS_HOST_GATE", "0")
     return request.param
