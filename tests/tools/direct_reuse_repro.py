@@ -1,4 +1,4 @@
-"""Debug aid: synchronous direct calls over a FRESH buffer each iteration,
+"""Debug aid: synchronous (staged) calls over a FRESH buffer each iteration,
 the previous one freed first (numpy -> munmap), so a new buffer often lands
 at the same virtual addresses as the last one, now backed by other physical
 pages. Checks every call against the oracle and reports address reuse and
