@@ -261,13 +261,10 @@ size_t batch_span(size_t nstripes, size_t stripe_stride, int rows, size_t row_st
   return (nstripes - 1) * stripe_stride + static_cast<size_t>(rows - 1) * row_stride + len;
 }
 
-size_t hbatch_target_bytes() {
-  static const size_t v = [] {
-    const char* e = getenv("HRS_HBATCH_BYTES");
-    long x = e ? atol(e) : 0;
-    return static_cast<size_t>(x > 0 ? x : 48l << 20);  // device image per chunk
-  }();
-  return v;
+size_t hbatch_target_bytes() {  // read per call (A/B runs in one process)
+  const char* e = getenv("HRS_HBATCH_BYTES");
+  const long x = e ? atol(e) : 0;
+  return static_cast<size_t>(x > 0 ? x : 48l << 20);  // device image per chunk
 }
 
 // H2D and D2H on their own streams (one per direction, shared by the slots),
@@ -406,21 +403,21 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
     bool used = false;  // the slot's events have been recorded by this call
     size_t s0 = 0, ns = 0;
   } pend[hrs::kHostBatchSlots];
-  // pageable: wait for a slot, then copy its outputs out of staging
+  // wait for a slot; pageable: queue the copies of its outputs out of
+  // staging in `jobs` (the caller runs them, merged with the slot's next
+  // copy-in: the output block and the input image are disjoint)
   auto finish = [&](int sl) -> hrs_status {
     if (!pend[sl].busy) return HRS_OK;
     hrs_codec::HostBatchSlot& h = c->hbatch[sl];
     hipError_t e = hipEventSynchronize(h.done);
     if (e != hipSuccess) return hip_fail(c, e, "hipEventSynchronize");
     if (!pinned) {
-      jobs.clear();
       const uint8_t* pout = h.pin + chunk * img_stripe;
       for (size_t i = 0; i < pend[sl].ns; ++i) {
         const size_t s = pend[sl].s0 + i;
         for (int t = 0; t < writes(s); ++t)
           jobs.push_back({hout + s * out_stripe + t * out_row, pout + i * out_stripe_dev + t * dpitch, len});
       }
-      pool.run(jobs);
     }
     pend[sl].busy = false;
     return HRS_OK;
@@ -431,9 +428,9 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
     hrs_codec::HostBatchSlot& h = c->hbatch[sl];
     const size_t ns = std::min(chunk, nstripes - s0);
     if (!pinned) {
+      jobs.clear();
       hrs_status st = finish(sl);
       if (st != HRS_OK) return st;
-      jobs.clear();
       for (size_t i = 0; i < ns; ++i)
         for (const RowRun& r : reads(s0 + i))
           for (int q = 0; q < r.cnt; ++q) {
@@ -493,9 +490,11 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
     pend[sl].s0 = s0;
     pend[sl].ns = ns;
   }
-  for (int sl = 0; sl < hrs::kHostBatchSlots; ++sl) {
-    hrs_status st = finish(sl);
+  for (int k = 1; k <= hrs::kHostBatchSlots; ++k) {  // in chunk order
+    jobs.clear();
+    hrs_status st = finish(static_cast<int>((j + k - 1) % hrs::kHostBatchSlots));
     if (st != HRS_OK) return st;
+    if (!jobs.empty()) pool.run(jobs);
   }
   return HRS_OK;
 }

@@ -6,6 +6,7 @@ A/B, interleaved rep by rep in one process:
            (pinned callers: one launch over the caller's stripes; pageable:
            over the slots' pinned staging), default
   zc_bN    zc with the grid capped at N blocks (HRS_ZC_BLOCKS=N; default 64)
+  zc_24m / zc_96m  chunk device image 24 / 96 MiB (HRS_HBATCH_BYTES; default 48)
 Workload = BASELINE configs[4] per GPU: RS(12,4), 256 KiB cells, 512 stripes,
 a seeded random lost pair per stripe; pinned and pageable host memory.
 
@@ -28,6 +29,7 @@ import synth  # noqa: E402
 from lambdafs_amd import HipReedSolomonCode, device  # noqa: E402
 
 GiB = float(1 << 30)
+KNOBS = ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS", "HRS_HBATCH_BYTES")
 
 
 def main():
@@ -62,13 +64,14 @@ def main():
         "encode_pageable": lambda: device.encode_batch_host(code, pge),
     }
     modes = {"ring": {"HRS_ZEROCOPY": "0"}, "duplex": {"HRS_ZEROCOPY": "0", "HRS_HBATCH_DUPLEX": "1"},
-             "zc": {}, "zc_uncapped": {"HRS_ZC_BLOCKS": "0"}}
+             "zc": {}, "zc_uncapped": {"HRS_ZC_BLOCKS": "0"},
+             "zc_24m": {"HRS_HBATCH_BYTES": str(24 << 20)}, "zc_96m": {"HRS_HBATCH_BYTES": str(96 << 20)}}
     for b in args.zc_blocks:
         modes[f"zc_b{b}"] = {"HRS_ZC_BLOCKS": str(b)}
     res = {m: {leg: [] for leg in legs} for m in modes}
     for r in range(args.reps + 1):
         for m, env in modes.items():
-            for key in ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS"):
+            for key in KNOBS:
                 os.environ.pop(key, None)
             os.environ.update(env)
             for leg, fn in legs.items():
@@ -89,7 +92,7 @@ def main():
                     raise RuntimeError(f"{m} {leg}: output differs")
                 outn[:] = 0
                 pout[:] = 0
-    for key in ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS"):
+    for key in KNOBS:
         os.environ.pop(key, None)
     line = {"workload": f"RS({k},{p}) {L >> 10} KiB cells x {S} stripes, random lost pair per stripe",
             "bit_exact": True}
