@@ -267,6 +267,14 @@ size_t hbatch_target_bytes() {  // read per call (A/B runs in one process)
   return static_cast<size_t>(x > 0 ? x : 48l << 20);  // device image per chunk
 }
 
+// A staged batch's copy-out of a finished slot goes to the copy pool in one
+// batch with the slot's next copy-in (HRS_HBATCH_MERGE=0: two batches, the
+// round-5 form; read per call, A/B runs).
+bool hbatch_merge() {
+  const char* e = getenv("HRS_HBATCH_MERGE");
+  return !(e && e[0] == '0');
+}
+
 // H2D and D2H on their own streams (one per direction, shared by the slots),
 // or on each slot's stream behind and ahead of its kernels (HRS_HBATCH_DUPLEX=0:
 // the round-3 pipeline, kept for A/B runs; read per call so one process can
@@ -398,6 +406,7 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
   const uint8_t nt = host_store_mode();
   std::vector<hrs::CopyJob> jobs;
   const bool duplex = hbatch_duplex();
+  const bool merge = hbatch_merge();
   struct Pending {
     bool busy = false;
     bool used = false;  // the slot's events have been recorded by this call
@@ -431,6 +440,10 @@ hrs_status host_batch(hrs_codec* c, const uint8_t* hin, size_t in_row, size_t in
       jobs.clear();
       hrs_status st = finish(sl);
       if (st != HRS_OK) return st;
+      if (!merge && !jobs.empty()) {
+        pool.run(jobs);
+        jobs.clear();
+      }
       for (size_t i = 0; i < ns; ++i)
         for (const RowRun& r : reads(s0 + i))
           for (int q = 0; q < r.cnt; ++q) {

@@ -7,6 +7,7 @@ A/B, interleaved rep by rep in one process:
            over the slots' pinned staging), default
   zc_bN    zc with the grid capped at N blocks (HRS_ZC_BLOCKS=N; default 64)
   zc_24m / zc_96m  chunk device image 24 / 96 MiB (HRS_HBATCH_BYTES; default 48)
+  zc_nomerge  a slot's copy-out and the next copy-in as two pool batches (HRS_HBATCH_MERGE=0)
 Workload = BASELINE configs[4] per GPU: RS(12,4), 256 KiB cells, 512 stripes,
 a seeded random lost pair per stripe; pinned and pageable host memory.
 
@@ -29,7 +30,7 @@ import synth  # noqa: E402
 from lambdafs_amd import HipReedSolomonCode, device  # noqa: E402
 
 GiB = float(1 << 30)
-KNOBS = ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS", "HRS_HBATCH_BYTES")
+KNOBS = ("HRS_ZEROCOPY", "HRS_HBATCH_DUPLEX", "HRS_ZC_BLOCKS", "HRS_HBATCH_BYTES", "HRS_HBATCH_MERGE")
 
 
 def main():
@@ -65,7 +66,8 @@ def main():
     }
     modes = {"ring": {"HRS_ZEROCOPY": "0"}, "duplex": {"HRS_ZEROCOPY": "0", "HRS_HBATCH_DUPLEX": "1"},
              "zc": {}, "zc_uncapped": {"HRS_ZC_BLOCKS": "0"},
-             "zc_24m": {"HRS_HBATCH_BYTES": str(24 << 20)}, "zc_96m": {"HRS_HBATCH_BYTES": str(96 << 20)}}
+             "zc_24m": {"HRS_HBATCH_BYTES": str(24 << 20)}, "zc_96m": {"HRS_HBATCH_BYTES": str(96 << 20)},
+             "zc_nomerge": {"HRS_HBATCH_MERGE": "0"}}
     for b in args.zc_blocks:
         modes[f"zc_b{b}"] = {"HRS_ZC_BLOCKS": str(b)}
     res = {m: {leg: [] for leg in legs} for m in modes}
