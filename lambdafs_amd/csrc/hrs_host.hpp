@@ -19,9 +19,11 @@
 // complex (CCD) it runs on, about 70 GB/s each; threads on distinct CCDs add
 // up (4 threads copying a 2.5 MiB chunk: 188 GB/s on one L3, 271 GB/s over
 // four). So each worker is bound to the CPUs of its own L3 within the
-// process's affinity set, away from the constructing thread's L3, on its NUMA
-// node first (HRS_HOST_PIN=0: no binding). With an affinity set inside one L3
-// nothing is bound.
+// process's affinity set, away from the constructing thread's L3, on the
+// GPU's NUMA node first, where the pinned staging lives (set_home_node;
+// HRS_HOST_HOME=caller: the constructing thread's node), the GPU ordinal
+// choosing where on that node's L3s a process starts (HRS_HOST_PIN=0: no
+// binding). With an affinity set inside one L3 nothing is bound.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -63,6 +65,13 @@ struct CopyJob {
 inline std::atomic<int>& pool_home_node() {
   static std::atomic<int> node{-1};
   return node;
+}
+
+// The GPU's ordinal, so processes driving different GPUs of one node start
+// their workers on different L3s of it (one process per GPU).
+inline std::atomic<int>& pool_home_ordinal() {
+  static std::atomic<int> ordinal{0};
+  return ordinal;
 }
 
 // NUMA node of the CPU the calling thread runs on, -1 if unknown.
@@ -120,9 +129,10 @@ class CopyPool {
 
   // The GPU's NUMA node, for the workers' placement (first caller wins; call
   // before the pool's first use for it to count).
-  static void set_home_node(int node) {
+  static void set_home_node(int node, int ordinal = 0) {
     int none = -1;
-    if (node >= 0) pool_home_node().compare_exchange_strong(none, node);
+    if (node >= 0 && pool_home_node().compare_exchange_strong(none, node))
+      pool_home_ordinal().store(ordinal > 0 ? ordinal : 0);
   }
 
   void run(const std::vector<CopyJob>& jobs) {
@@ -273,9 +283,9 @@ class CopyPool {
 
   // One CPU set per worker: the allowed CPUs of one L3 each, the L3s on the
   // home NUMA node first (the GPU's, set_home_node; HRS_HOST_HOME=caller or no
-  // home: the constructing thread's node), the constructing thread's own L3
-  // last. Empty when the affinity set spans fewer than two L3s or sysfs says
-  // nothing.
+  // home: the constructing thread's node) starting at the GPU ordinal's n-th,
+  // the constructing thread's own L3 last. Empty when the affinity set spans
+  // fewer than two L3s or sysfs says nothing.
   static std::vector<cpu_set_t> worker_homes(int n) {
     std::vector<cpu_set_t> homes;
     cpu_set_t set;
@@ -311,6 +321,12 @@ class CopyPool {
     }
     std::stable_sort(order.begin(), order.end(),
                      [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
+    // the wanted node's L3s from the GPU ordinal's n-th one on: with one
+    // process per GPU, the pools of a node's GPUs spread over its L3s
+    const int nwant = static_cast<int>(std::count_if(order.begin(), order.end(),
+                                                     [](const std::pair<int, int>& o) { return o.first == 0; }));
+    if (nwant > 1)
+      std::rotate(order.begin(), order.begin() + (pool_home_ordinal().load() * n) % nwant, order.begin() + nwant);
     for (int i = 0; i < n && i < static_cast<int>(order.size()); ++i) {
       cpu_set_t h;
       CPU_ZERO(&h);

@@ -236,7 +236,7 @@ static int device_numa_node(hrs_codec* c) {
 }
 
 hrs::CopyPool& copy_pool(hrs_codec* c) {
-  hrs::CopyPool::set_home_node(device_numa_node(c));
+  hrs::CopyPool::set_home_node(device_numa_node(c), c->device);
   return hrs::CopyPool::instance();
 }
 
