@@ -44,6 +44,12 @@ def main():
         return round(float(np.median(ms)), 3)
 
     res = {}
+    hold_gib = int(os.environ.get("PROBE_HOLD_GIB", "0"))  # device memory held, as bench.py's workload does
+    held = torch.empty(hold_gib << 30, dtype=torch.uint8, device="cuda") if hold_gib else None
+    if held is not None:
+        held.fill_(1)
+        torch.cuda.synchronize()
+    res["held_gib"] = hold_gib
     pg = np.array(stn)
     pout = np.zeros((S, 2, L), np.uint8)
     dec = lambda: device.decode_batch_host(code, pg, er, pout)  # noqa: E731
