@@ -13,4 +13,4 @@ ON=$((1 - GN))
 OC=$(cat /sys/devices/system/node/node$ON/cpulist)
 echo "gpu_node(guess)=$GN other_cpus=$OC" > $O/placement.txt
 timeout -k 10 300 taskset -c $OC python -u tests/tools/fuzz_long.py 4 1000 > $O/fuzz_other.jsonl 2> $O/fuzz_other.err
-timeout -k 10 300 python -u tests/tools/direct_reuse_repro.py 400 > $O/reuse.txt 2> $O/reuse.err
+timeout -k 10 300 python -u tests/tools/fresh_buffer_repro.py 400 > $O/reuse.txt 2> $O/reuse.err

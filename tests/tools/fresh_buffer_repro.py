@@ -2,7 +2,7 @@
 the previous one freed first (numpy -> munmap), so a new buffer often lands
 at the same virtual addresses as the last one, now backed by other physical
 pages. Checks every call against the oracle and reports address reuse and
-mismatches. Usage: python tests/tools/direct_reuse_repro.py [iters] [gap]"""
+mismatches. Usage: python tests/tools/fresh_buffer_repro.py [iters] [gap]"""
 import os
 import sys
 
