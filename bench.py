@@ -204,6 +204,29 @@ def cpu_baseline(k, p, L, nstripes, threads=None):
     }
 
 
+def placement(local):
+    """NUMA node of the CPU the calling thread runs on and of the GPU's PCI
+    function (sysfs): a staged call from the GPU's socket is ~10-20 us faster
+    than from the other one (profiles/r06/NOTES.md §4). None where unknown."""
+    out = {"caller_node": None, "gpu_node": None}
+    try:
+        import ctypes
+        cpu = ctypes.CDLL(None).sched_getcpu()
+        for name in os.listdir(f"/sys/devices/system/cpu/cpu{cpu}"):
+            if name.startswith("node") and name[4:].isdigit():
+                out["caller_node"] = int(name[4:])
+    except (OSError, AttributeError, ValueError):
+        pass
+    try:
+        pr = torch.cuda.get_device_properties(local)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            out["gpu_node"] = int(f.read().strip())
+    except (OSError, AttributeError, ValueError, RuntimeError):
+        pass
+    return out
+
+
 def host_calls(local, calls=100):
     """The drop-in's synchronous call rate:
     one RS(10,4) stripe of 1 MiB pageable rows per call through the C ABI the
@@ -264,6 +287,7 @@ def host_calls(local, calls=100):
                           "path": code.lastHostPath()}
     ok &= all(np.array_equal(pin[r], rows[r]) for r in range(p))
     res["bit_exact"] = ok
+    res["placement"] = placement(local)
     if not ok:
         raise RuntimeError("host-buffer decode did not reproduce the lost row")
     return res
